@@ -1,0 +1,128 @@
+/*
+ * xa_common.h -- block geometry and arithmetic shared by the gfx950 kernels.
+ *
+ * Format facts (reference src/libbjxa.c):
+ *   channel block = 1 profile byte + bits*4 data bytes            (:431)
+ *   effective block (eblock) = L block [+ R block], 32 frames     (:629-646)
+ *   profile = gain<<4 | range; gain >= 5 is a protocol error      (:547-550)
+ *   K0/K1 x 256 per gain                                          (:525-531)
+ */
+#ifndef BJXA_XA_COMMON_H
+#define BJXA_XA_COMMON_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define XA_FRAMES 32
+
+/* channel block / effective block sizes in bytes */
+template <int BITS> struct xa_bits {
+	static constexpr int BSZ = BITS * 4 + 1;
+	/* a "group" is 4 channel blocks (4 mono blocks or 2 stereo eblocks):
+	 * 4*BSZ bytes = BSZ dwords, always 4-byte aligned */
+	static constexpr int GDW = BSZ;
+};
+
+/*
+ * K0 (9 bits, unsigned) and |K1| (8 bits) packed per gain so a lane can pick
+ * its block's pair with two shifts instead of a table load.  Gains 5-7 (the
+ * error case) map to 0/0; their output is never emitted.
+ */
+__device__ __forceinline__ void
+xa_gain(uint32_t gain, int32_t &k0, int32_t &k1)
+{
+	const uint64_t K0 = (0ull) | (240ull << 9) | (460ull << 18) |
+	    (392ull << 27) | (488ull << 36);
+	const uint64_t K1 = (0ull) | (0ull << 8) | (208ull << 16) |
+	    (220ull << 24) | (240ull << 32);
+	k0 = (int32_t)((K0 >> (gain * 9)) & 511u);
+	k1 = -(int32_t)((K1 >> (gain * 8)) & 255u);
+}
+
+/*
+ * One predictor step (src/libbjxa.c:556-572):
+ *   s = clamp(t + trunc((p0*K0 + p1*K1) / 256))
+ * `top` holds the unpacked code left-justified at bit 31 with zeros below
+ * bit 16, so t = top >> (16 + range) equals (int16 code) >> range.
+ * The truncating divide is floor((g + 255*[g<0]) / 256).
+ */
+__device__ __forceinline__ int32_t
+xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
+    int32_t &p1)
+{
+	int32_t t = top >> sh;
+	int32_t g = __mul24(p0, k0) + __mul24(p1, k1);
+	int32_t s = t + ((g + (int32_t)((uint32_t)(g >> 31) >> 24)) >> 8);
+	s = min(max(s, -32768), 32767);
+	p1 = p0;
+	p0 = s;
+	return s;
+}
+
+/*
+ * The helpers below take byte/code indices as plain ints: every call site
+ * sits inside fully unrolled loops, so the indices fold to constants and
+ * w[] stays in VGPRs (checked: no scratch in the kernel resource usage).
+ */
+
+/* byte b of the dword array, moved to bits 24..31, zeros below */
+__device__ __forceinline__ uint32_t
+xa_byte_top(const uint32_t *w, const int b)
+{
+	return __builtin_amdgcn_perm(0u, w[b >> 2], 0x0c0c0c0cu |
+	    ((uint32_t)(b & 3) << 24));
+}
+
+/* bytes b (-> bits 24..31) and b+1 (-> bits 16..23) */
+__device__ __forceinline__ uint32_t
+xa_2bytes_top(const uint32_t *w, const int b)
+{
+	if ((b >> 2) == ((b + 1) >> 2)) {
+		return __builtin_amdgcn_perm(0u, w[b >> 2], 0x0c0c0000u |
+		    ((uint32_t)(b & 3) << 24) | ((uint32_t)((b + 1) & 3) << 16));
+	}
+	/* b is byte 3 of w[i], b+1 is byte 0 of w[i+1]; v_perm_b32 indexes
+	 * the 64-bit {S0, S1}: selectors 0-3 pick bytes of S1 (w[i]),
+	 * 4-7 bytes of S0 (w[i+1]) */
+	return __builtin_amdgcn_perm(w[(b + 1) >> 2], w[b >> 2],
+	    0x0c0c0000u | (3u << 24) | (4u << 16));
+}
+
+/*
+ * Code n (0..31) of the channel block whose profile byte is byte o of w,
+ * left-justified: bits 31..16 hold the reference's int16 inflate value
+ * (src/libbjxa.c:286-345), lower bits are zero.
+ */
+template <int BITS>
+__device__ __forceinline__ int32_t
+code_at(const uint32_t *w, const int o, const int n)
+{
+	if (BITS == 8)
+		return (int32_t)xa_byte_top(w, o + 1 + n);
+	if (BITS == 4) {
+		/* high nibble first (src/libbjxa.c:295-298) */
+		uint32_t v = xa_byte_top(w, o + 1 + n / 2);
+		return (int32_t)((n & 1) ? (v << 4) : (v & 0xf0000000u));
+	}
+	/* 6-bit: 4 codes per 3 bytes, big-endian (src/libbjxa.c:315-321) */
+	const int bit = 6 * n, byte = bit >> 3, off = bit & 7;
+	uint32_t v = off <= 2 ? xa_byte_top(w, o + 1 + byte) :
+	    xa_2bytes_top(w, o + 1 + byte);
+	return (int32_t)((v << off) & 0xfc000000u);
+}
+
+/* state word: p0 in bits 0..15, p1 in bits 16..31 */
+__device__ __forceinline__ uint32_t
+xa_pack_state(int32_t p0, int32_t p1)
+{
+	return ((uint32_t)p0 & 0xffffu) | ((uint32_t)p1 << 16);
+}
+
+__device__ __forceinline__ void
+xa_unpack_state(uint32_t s, int32_t &p0, int32_t &p1)
+{
+	p0 = (int32_t)(int16_t)(s & 0xffffu);
+	p1 = (int32_t)(int16_t)(s >> 16);
+}
+
+#endif

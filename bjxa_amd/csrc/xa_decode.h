@@ -1,0 +1,52 @@
+/*
+ * xa_decode.h -- kernel argument block and workspace layout (internal).
+ */
+#ifndef BJXA_XA_DECODE_H
+#define BJXA_XA_DECODE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+/* workspace control words (reset by the tail kernel after every call) */
+#define XA_CTL_ERR	0	/* min channel-block index with gain >= 5 */
+#define XA_CTL_NQ	1	/* re-check queue length */
+#define XA_CTL_FIXED	2	/* chunks repaired by K2 */
+#define XA_CTL_WORDS	64	/* 256 B */
+
+/* status words written by the tail kernel */
+#define XA_ST_ERR	0
+#define XA_ST_STATE_L	1
+#define XA_ST_STATE_R	2
+#define XA_ST_FIXED	3
+#define XA_ST_TAIL	4
+#define XA_ST_CHUNKS	5
+#define XA_ST_WORDS	8
+
+struct xa_dec_args {
+	const uint8_t *src;	/* XA blocks, eblock b at src + b*ch*(bits*4+1) */
+	uint8_t *dst;		/* PCM, eblock b at dst + b*64*ch */
+	uint64_t pcm_bytes;	/* PCM bytes to emit (last block may be cut) */
+	uint32_t eblocks;
+	uint32_t nchunks;
+	uint32_t C, W;		/* chunk and warm-up lengths in eblocks */
+	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
+	uint2 *g, *e;		/* per-chunk entry / exit state */
+	uint32_t *queue;	/* re-check queue, nchunks entries */
+	uint32_t *ctl;		/* XA_CTL_WORDS */
+	uint32_t *status;	/* XA_ST_WORDS */
+};
+
+hipError_t xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
+    hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+
+struct xa_enc_args {
+	const uint8_t *src;	/* PCM frames, 16-bit, channels interleaved */
+	uint8_t *dst;		/* XA blocks */
+	uint64_t frames;	/* valid frames; the last block is zero-padded */
+	uint32_t eblocks;	/* ceil(frames / 32) */
+};
+
+hipError_t xa_encode_launch(const xa_enc_args &a, unsigned bits, unsigned ch,
+    hipStream_t st);
+
+#endif

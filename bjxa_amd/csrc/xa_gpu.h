@@ -1,0 +1,40 @@
+/*
+ * xa_gpu.h -- internal interface between the host C library (libbjxa.c)
+ * and the HIP translation units.  Local symbols; not part of the ABI.
+ */
+#ifndef BJXA_XA_GPU_H
+#define BJXA_XA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct bjxa__gpu;
+
+/* NULL + errno (ENODEV without a GPU, ENOMEM) on failure */
+struct bjxa__gpu *bjxa__gpu_new(void);
+void bjxa__gpu_free(struct bjxa__gpu *g);
+
+/*
+ * Decode `eblocks` effective blocks from host `src`, starting in `state`
+ * (L p0, L p1, R p0, R p1); copy the first `dst_bytes` PCM bytes to host
+ * `dst`.  *err_cb is the first failing channel block (eblock*ch + channel)
+ * or 0xffffffff; on failure only the eblocks before it are copied and
+ * `state` is the state at that point.  Returns 0 or -1/errno.
+ */
+int bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
+    unsigned bits, unsigned ch, int16_t state[4], void *dst,
+    uint64_t dst_bytes, uint32_t *err_cb);
+
+/* encode `frames` frames from host `src` into ceil(frames/32) eblocks */
+int bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
+    unsigned bits, unsigned ch, void *dst);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

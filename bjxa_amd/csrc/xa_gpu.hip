@@ -1,0 +1,354 @@
+/*
+ * xa_gpu.hip -- C-ABI around the gfx950 kernels.
+ *
+ *  - bjxa_hip_* (include/bjxa_hip.h): device-resident entry points.
+ *  - bjxa__gpu_* (xa_gpu.h): what the host C library (libbjxa.c) calls from
+ *    bjxa_decode()/bjxa_encode() -- the reference's hot-path entries
+ *    (src/libbjxa.c:602-661, :759-819) -- to run one call on the GPU.
+ *    These are local symbols (libbjxa.map).
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "xa_decode.h"
+#include "xa_gpu.h"
+#include "../../include/bjxa_hip.h"
+
+#define DEFAULT_WARMUP	8u	/* eblocks; SURVEY App. C / DESIGN.md */
+#define TARGET_LANES	(256u * 12u * 64u)
+
+static int
+gpu_present(void)
+{
+	static int state;	/* 0 unknown, 1 yes, -1 no */
+	if (state == 0) {
+		int n = 0;
+		state = (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : -1;
+	}
+	return state > 0;
+}
+
+static uint32_t
+round_up(uint32_t v, uint32_t m)
+{
+	return (v + m - 1) / m * m;
+}
+
+static void
+pick_tuning(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
+    uint32_t *C, uint32_t *W)
+{
+	const uint32_t G = 4 / ch;
+	uint32_t c = t && t->chunk ? t->chunk : 0;
+	uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup : DEFAULT_WARMUP;
+	if (c == 0) {
+		c = (eblocks + TARGET_LANES - 1) / TARGET_LANES;
+		if (c < 16)
+			c = 16;
+	}
+	*C = round_up(c, G);
+	*W = round_up(w, G);
+}
+
+static size_t
+ws_bytes(uint32_t nchunks)
+{
+	return XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 4) + 64;
+}
+
+extern "C" size_t
+bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
+    const bjxa_hip_tuning_t *tune)
+{
+	uint32_t C, W;
+	if (channels != 1 && channels != 2)
+		return 0;
+	pick_tuning(eblocks, channels, tune, &C, &W);
+	return ws_bytes((eblocks + C - 1) / C);
+}
+
+__global__ void
+xa_ws_init(uint32_t *ctl)
+{
+	if (threadIdx.x < XA_CTL_WORDS)
+		ctl[threadIdx.x] = threadIdx.x == XA_CTL_ERR ? 0xffffffffu : 0u;
+}
+
+extern "C" int
+bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream)
+{
+	if (d_ws == NULL || ws_len < XA_CTL_WORDS * 4) {
+		errno = EINVAL;
+		return -1;
+	}
+	if (!gpu_present()) {
+		errno = ENODEV;
+		return -1;
+	}
+	hipLaunchKernelGGL(xa_ws_init, dim3(1), dim3(64), 0,
+	    (hipStream_t)stream, (uint32_t *)d_ws);
+	if (hipGetLastError() != hipSuccess) {
+		errno = EIO;
+		return -1;
+	}
+	return 0;
+}
+
+extern "C" int
+bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
+    uint32_t *d_status, const bjxa_hip_tuning_t *tune, void *stream)
+{
+	uint32_t C, W;
+	if (s == NULL || d_ws == NULL || d_status == NULL || s->d_src == NULL ||
+	    s->d_dst == NULL || (s->bits != 4 && s->bits != 6 && s->bits != 8) ||
+	    (s->channels != 1 && s->channels != 2) || s->eblocks == 0 ||
+	    s->frames > (uint64_t)s->eblocks * 32u ||
+	    s->frames <= (uint64_t)(s->eblocks - 1) * 32u ||
+	    ((uintptr_t)s->d_src & 3u) != 0 || ((uintptr_t)s->d_dst & 15u) != 0 ||
+	    ((uintptr_t)d_ws & 15u) != 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	if (!gpu_present()) {
+		errno = ENODEV;
+		return -1;
+	}
+	pick_tuning(s->eblocks, s->channels, tune, &C, &W);
+	xa_dec_args a;
+	a.src = (const uint8_t *)s->d_src;
+	a.dst = (uint8_t *)s->d_dst;
+	a.pcm_bytes = s->frames * 2u * s->channels;
+	a.eblocks = s->eblocks;
+	a.nchunks = (s->eblocks + C - 1) / C;
+	a.C = C;
+	a.W = W;
+	a.init[0] = ((uint32_t)(uint16_t)s->state[0]) |
+	    ((uint32_t)(uint16_t)s->state[1] << 16);
+	a.init[1] = ((uint32_t)(uint16_t)s->state[2]) |
+	    ((uint32_t)(uint16_t)s->state[3] << 16);
+	if (ws_len < ws_bytes(a.nchunks)) {
+		errno = EINVAL;
+		return -1;
+	}
+	uint8_t *ws = (uint8_t *)d_ws;
+	a.ctl = (uint32_t *)ws;
+	a.g = (uint2 *)(ws + XA_CTL_WORDS * 4);
+	a.e = a.g + a.nchunks;
+	a.queue = (uint32_t *)(a.e + a.nchunks);
+	a.status = d_status;
+	if (xa_decode_launch(a, s->bits, s->channels, (hipStream_t)stream,
+	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
+	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
+		errno = EIO;
+		return -1;
+	}
+	return 0;
+}
+
+extern "C" int
+bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
+    unsigned channels, void *d_xa, void *stream)
+{
+	if (d_pcm == NULL || d_xa == NULL || frames == 0 ||
+	    (bits != 4 && bits != 6 && bits != 8) ||
+	    (channels != 1 && channels != 2) || (frames + 31) / 32 > 0xffffffffu ||
+	    ((uintptr_t)d_pcm & 15u) != 0 || ((uintptr_t)d_xa & 3u) != 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	if (!gpu_present()) {
+		errno = ENODEV;
+		return -1;
+	}
+	xa_enc_args a;
+	a.src = (const uint8_t *)d_pcm;
+	a.dst = (uint8_t *)d_xa;
+	a.frames = frames;
+	a.eblocks = (uint32_t)((frames + 31) / 32);
+	if (xa_encode_launch(a, bits, channels, (hipStream_t)stream) !=
+	    hipSuccess) {
+		errno = EIO;
+		return -1;
+	}
+	return 0;
+}
+
+extern "C" const char *
+bjxa_hip_version(void)
+{
+	return "bjxa-mi355x 0.1 gfx950 (spec/fix/tail decode, group encode)";
+}
+
+/* ------------------------------------------------------------------ */
+/* per-codec GPU context behind bjxa_decode()/bjxa_encode()            */
+
+struct bjxa__gpu {
+	hipStream_t	stream;
+	void		*d_in, *d_out, *d_ws;
+	size_t		in_cap, out_cap, ws_cap;
+	uint32_t	*d_status;
+};
+
+static int
+grow(void **p, size_t *cap, size_t need)
+{
+	if (*cap >= need)
+		return 0;
+	if (*p != NULL)
+		(void)hipFree(*p);
+	*p = NULL;
+	*cap = 0;
+	need = (need + 4095) & ~(size_t)4095;
+	if (hipMalloc(p, need) != hipSuccess) {
+		*p = NULL;
+		errno = ENOMEM;
+		return -1;
+	}
+	*cap = need;
+	return 0;
+}
+
+extern "C" struct bjxa__gpu *
+bjxa__gpu_new(void)
+{
+	if (!gpu_present()) {
+		errno = ENODEV;
+		return NULL;
+	}
+	struct bjxa__gpu *g = (struct bjxa__gpu *)calloc(1, sizeof *g);
+	if (g == NULL) {
+		errno = ENOMEM;
+		return NULL;
+	}
+	if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) !=
+	    hipSuccess || hipMalloc((void **)&g->d_status, 64) != hipSuccess) {
+		free(g);
+		errno = ENODEV;
+		return NULL;
+	}
+	return g;
+}
+
+extern "C" void
+bjxa__gpu_free(struct bjxa__gpu *g)
+{
+	if (g == NULL)
+		return;
+	(void)hipStreamSynchronize(g->stream);
+	(void)hipFree(g->d_in);
+	(void)hipFree(g->d_out);
+	(void)hipFree(g->d_ws);
+	(void)hipFree(g->d_status);
+	(void)hipStreamDestroy(g->stream);
+	free(g);
+}
+
+static int
+io_fail(void)
+{
+	errno = EIO;
+	return -1;
+}
+
+extern "C" int
+bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
+    unsigned bits, unsigned ch, int16_t state[4], void *dst,
+    uint64_t dst_bytes, uint32_t *err_cb)
+{
+	const size_t ebsz = (size_t)(bits * 4 + 1) * ch;
+	const size_t in_bytes = ebsz * eblocks;
+	const size_t out_full = (size_t)eblocks * 64u * ch;
+	bjxa_hip_stream_t s;
+	uint32_t st[BJXA_HIP_STATUS_WORDS];
+	int fresh = g->d_ws == NULL;
+
+	size_t wsn = bjxa_hip_decode_workspace(eblocks, ch, NULL);
+	if (grow(&g->d_in, &g->in_cap, in_bytes + 16) < 0 ||
+	    grow(&g->d_out, &g->out_cap, out_full) < 0)
+		return -1;
+	if (g->ws_cap < wsn) {
+		if (grow(&g->d_ws, &g->ws_cap, wsn) < 0)
+			return -1;
+		fresh = 1;
+	}
+	if (fresh && bjxa_hip_workspace_init(g->d_ws, g->ws_cap, g->stream) < 0)
+		return -1;
+	if (hipMemcpyAsync(g->d_in, src, in_bytes, hipMemcpyHostToDevice,
+	    g->stream) != hipSuccess)
+		return io_fail();
+	s.d_src = g->d_in;
+	s.d_dst = g->d_out;
+	s.eblocks = eblocks;
+	s.frames = (uint64_t)eblocks * 32u;	/* full blocks on the device */
+	s.bits = (uint8_t)bits;
+	s.channels = (uint8_t)ch;
+	memcpy(s.state, state, sizeof s.state);
+	if (bjxa_hip_decode_async(&s, g->d_ws, g->ws_cap, g->d_status, NULL,
+	    g->stream) < 0)
+		return -1;
+	if (hipMemcpyAsync(st, g->d_status, sizeof st, hipMemcpyDeviceToHost,
+	    g->stream) != hipSuccess || hipStreamSynchronize(g->stream) !=
+	    hipSuccess)
+		return io_fail();
+	*err_cb = st[XA_ST_ERR];
+	if (st[XA_ST_ERR] != 0xffffffffu) {
+		/* stop before the failing eblock, as the reference does; the
+		 * left channel of that eblock is already advanced if the right
+		 * block is the bad one (src/libbjxa.c:633-643) */
+		const uint32_t j = st[XA_ST_ERR] / ch, bad_c = st[XA_ST_ERR] % ch;
+		int16_t fr[2][2];	/* frames 30, 31 */
+		if (dst_bytes > (size_t)j * 64u * ch)
+			dst_bytes = (size_t)j * 64u * ch;
+		if (j > 0) {
+			if (hipMemcpy(fr, (uint8_t *)g->d_out + ((size_t)j * 64u *
+			    ch) - 4u * ch, 4u * ch, hipMemcpyDeviceToHost) !=
+			    hipSuccess)
+				return io_fail();
+			for (unsigned c = 0; c < ch; c++) {
+				state[2 * c] = ch == 2 ? fr[1][c] : ((int16_t *)fr)[1];
+				state[2 * c + 1] = ch == 2 ? fr[0][c] : ((int16_t *)fr)[0];
+			}
+		}
+		if (ch == 2 && bad_c == 1) {
+			if (hipMemcpy(fr, (uint8_t *)g->d_out + ((size_t)(j + 1) *
+			    128u) - 8u, 8u, hipMemcpyDeviceToHost) != hipSuccess)
+				return io_fail();
+			state[0] = fr[1][0];
+			state[1] = fr[0][0];
+		}
+	} else {
+		state[0] = (int16_t)(st[XA_ST_STATE_L] & 0xffffu);
+		state[1] = (int16_t)(st[XA_ST_STATE_L] >> 16);
+		state[2] = (int16_t)(st[XA_ST_STATE_R] & 0xffffu);
+		state[3] = (int16_t)(st[XA_ST_STATE_R] >> 16);
+	}
+	if (dst_bytes > 0 && hipMemcpy(dst, g->d_out, dst_bytes,
+	    hipMemcpyDeviceToHost) != hipSuccess)
+		return io_fail();
+	return 0;
+}
+
+extern "C" int
+bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
+    unsigned bits, unsigned ch, void *dst)
+{
+	const size_t in_bytes = (size_t)frames * 2u * ch;
+	const uint32_t eblocks = (uint32_t)((frames + 31) / 32);
+	const size_t out_bytes = (size_t)eblocks * (bits * 4 + 1) * ch;
+
+	if (grow(&g->d_in, &g->in_cap, in_bytes + 256) < 0 ||
+	    grow(&g->d_out, &g->out_cap, out_bytes + 256) < 0)
+		return -1;
+	if (hipMemcpyAsync(g->d_in, src, in_bytes, hipMemcpyHostToDevice,
+	    g->stream) != hipSuccess)
+		return io_fail();
+	if (bjxa_hip_encode_async(g->d_in, frames, bits, ch, g->d_out,
+	    g->stream) < 0)
+		return -1;
+	if (hipMemcpyAsync(dst, g->d_out, out_bytes, hipMemcpyDeviceToHost,
+	    g->stream) != hipSuccess || hipStreamSynchronize(g->stream) !=
+	    hipSuccess)
+		return io_fail();
+	return 0;
+}

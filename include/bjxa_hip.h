@@ -1,0 +1,84 @@
+/*
+ * bjxa_hip.h -- device-resident extension of libbjxa (symbol version
+ * LIBBJXA_HIP_0.1).  New entry points only; nothing in bjxa.h changes.
+ *
+ * The reference has one hot-path entry per direction, bjxa_decode()
+ * (src/libbjxa.c:602-661) and bjxa_encode() (:759-819), both on host
+ * buffers, one stream at a time.  These entries take device pointers so a
+ * caller that keeps streams in HBM pays no PCIe copy, accept many streams
+ * per launch, and accept an explicit entry state -- the same thing the
+ * reference expresses through the befL/befR header fields (:417-420) to
+ * resume or segment a stream.
+ *
+ * All pointers named d_* are device pointers on the current HIP device;
+ * `stream` is a hipStream_t (NULL = default stream).  Calls are
+ * asynchronous; results are valid once the stream has been synchronized.
+ * Return: 0, or -1 with errno (EINVAL bad argument/alignment, ENODEV no
+ * GPU, EIO launch failure).
+ */
+#ifndef BJXA_HIP_H_INCLUDED
+#define BJXA_HIP_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* one stream to decode */
+typedef struct {
+	const void	*d_src;		/* XA blocks (no header), 4-B aligned */
+	void		*d_dst;		/* PCM out, 16-B aligned */
+	uint64_t	frames;		/* frames to emit: (eblocks-1)*32 <
+					 * frames <= eblocks*32 */
+	uint32_t	eblocks;	/* effective blocks */
+	uint8_t		bits;		/* 4, 6 or 8 */
+	uint8_t		channels;	/* 1 or 2 */
+	int16_t		state[4];	/* entry state: L prev[0], L prev[1],
+					 * R prev[0], R prev[1] */
+} bjxa_hip_stream_t;
+
+/* tuning and profiling hooks (zero/NULL = automatic/off) */
+typedef struct {
+	uint32_t	chunk;		/* eblocks per lane */
+	int32_t		warmup;		/* speculative warm-up eblocks, -1 = auto */
+	void		*ev_spec[2];	/* hipEvent_t pair recorded on `stream`
+					 * around the speculative-decode kernel */
+} bjxa_hip_tuning_t;
+
+/*
+ * Status written by a decode (8 x uint32, device memory):
+ *  [0] first failing channel block (eblock*channels + channel) whose gain
+ *      nibble is >= 5, 0xffffffff if none (the reference's EPROTO, :550)
+ *  [1] exit state L (prev[0] | prev[1] << 16)
+ *  [2] exit state R
+ *  [3] chunks repaired by the verify pass, [4] by the sequential tail,
+ *  [5] chunks
+ */
+#define BJXA_HIP_STATUS_WORDS 8
+
+/* workspace bytes for one stream of `eblocks`; zero it once (or call
+ * bjxa_hip_workspace_init) before first use; it is left reusable */
+size_t bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
+    const bjxa_hip_tuning_t *tune);
+int bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream);
+
+/* decode one stream (three kernels on `stream`, no host sync) */
+int bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws,
+    size_t ws_len, uint32_t *d_status, const bjxa_hip_tuning_t *tune,
+    void *stream);
+
+/* encode `frames` frames of 16-bit PCM into ceil(frames/32) XA eblocks
+ * (profile 0, last block zero-padded), d_pcm 16-B aligned, d_xa 4-B */
+int bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
+    unsigned channels, void *d_xa, void *stream);
+
+/* library/kernels build identifier, e.g. "bjxa-mi355x gfx950 ..." */
+const char *bjxa_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BJXA_HIP_H_INCLUDED */

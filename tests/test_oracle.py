@@ -1,0 +1,72 @@
+"""The CPU restatement (oracle/) against the reference's own known-answer
+vectors.  This is what makes the oracle a trustworthy parity checker."""
+import hashlib
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from bjxa_amd import synth
+
+
+@pytest.mark.parametrize("name", ["square-mono-4.xa", "square-mono-6.xa", "square-mono-8.xa",
+                                  "square-stereo-4.xa", "square-stereo-6.xa",
+                                  "square-stereo-8.xa"])
+def test_decode_fixture_sha1(name, manifest, golden):
+    """test/test_decode.sh:24-78 -- input and decoded-WAV SHA-1s."""
+    data = golden(name)
+    exp = manifest["fixtures"][name]
+    assert hashlib.sha1(data).hexdigest() == exp["xa_sha1"]
+    assert hashlib.sha1(oracle.decode_file(data)).hexdigest() == exp["wav_sha1"]
+
+
+def test_saturation_vector(manifest):
+    """test/test_decode.sh:80-122 -- the int16 clamp, both directions."""
+    b = bytes.fromhex(manifest["boundary"]["hex"])
+    wav = oracle.decode_file(b)
+    assert hashlib.sha1(wav).hexdigest() == manifest["boundary"]["wav_sha1"]
+    pcm = np.frombuffer(wav, dtype="<i2", offset=44).reshape(32, 2)
+    assert pcm[0, 0] == 32512 and (pcm[1:, 0] == 32767).all()
+    assert (pcm[:, 1] == -32768).all()
+
+
+@pytest.mark.parametrize("wav,bits", [(w, b) for w in ("square-mono.wav", "square-stereo.wav")
+                                      for b in (4, 6, 8)])
+def test_encode_fixture_sha1(wav, bits, manifest, golden):
+    """SURVEY.md App. B encode goldens (reference `bjxa encode --bits N`)."""
+    data = golden(wav)
+    ch, rate = struct.unpack("<HI", data[22:28])
+    dl = struct.unpack("<I", data[40:44])[0]
+    pcm = np.frombuffer(data, dtype="<i2", offset=44, count=dl // 2)
+    frames = dl // (2 * ch)
+    xa = oracle.encode(pcm, frames, bits, ch)
+    hdr = b"KWD1" + struct.pack("<IIHBBIhhhhI", xa.nbytes, frames, rate, bits, ch, 0, 0, 0, 0, 0, 0)
+    assert hashlib.sha1(hdr + xa.tobytes()).hexdigest() == manifest["encode"][wav][str(bits)]
+    # the reference's round-trip tolerance: decode(encode(x)) == x with the
+    # low 16-bits bits cleared
+    back, _, _, _ = oracle.decode(xa, (frames + 31) // 32, bits, ch, frames=frames)
+    assert np.array_equal(back, pcm & np.int16(~((1 << (16 - bits)) - 1)))
+
+
+def test_invalid_profile_semantics():
+    """test/test_decode_error.sh:221-282 -- decode stops at a gain >= 5."""
+    xa = synth.stream(8, 8, 2, "A", seed=3)
+    xa.reshape(16, 33)[5 * 2 + 1, 0] = 0x5F   # right block of eblock 5
+    pcm, st, done, bad = oracle.decode(xa, 8, 8, 2)
+    assert done == 5 and bad == 1
+    ref, _, _, _ = oracle.decode(xa, 5, 8, 2)
+    assert np.array_equal(pcm[:5 * 64], ref)
+
+
+def test_segmented_equals_single():
+    """Chaining segments through the carried state (the befL/befR trick of
+    src/libbjxa.c:417-420) equals one long decode."""
+    xa = synth.stream(3000, 6, 2, "W", seed=9)
+    whole, st_w, _, _ = oracle.decode(xa, 3000, 6, 2)
+    st = (0, 0, 0, 0)
+    parts = []
+    for a, b in ((0, 1000), (1000, 1001), (1001, 3000)):
+        p, st, _, _ = oracle.decode(xa[a * 50:b * 50], b - a, 6, 2, st)
+        parts.append(p)
+    assert np.array_equal(np.concatenate(parts), whole) and st == st_w
