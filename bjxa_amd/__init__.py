@@ -24,7 +24,8 @@ import struct
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbjxa.so.0")
+# BJXA_LIB_PATH selects an experimental build (tools/); default is in-tree
+LIB_PATH = os.environ.get("BJXA_LIB_PATH") or os.path.join(_HERE, "libbjxa.so.0")
 _lib = None
 
 STATUS_WORDS = 8
@@ -61,7 +62,7 @@ class HipStream(ctypes.Structure):
 
 class HipTuning(ctypes.Structure):
     _fields_ = [("chunk", ctypes.c_uint32), ("warmup", ctypes.c_int32),
-                ("ev_spec", ctypes.c_void_p * 2)]
+                ("ev_spec", ctypes.c_void_p * 2), ("variant", ctypes.c_uint32)]
 
 
 _P = ctypes.c_void_p
@@ -281,11 +282,12 @@ def workspace_init(d_ws, ws_len, stream=0):
 
 
 def decode_device(d_src, d_dst, eblocks, frames, bits, channels, d_ws, ws_len, d_status,
-                  state=(0, 0, 0, 0), chunk=0, warmup=-1, stream=0, events=(None, None)):
+                  state=(0, 0, 0, 0), chunk=0, warmup=-1, stream=0, events=(None, None),
+                  variant=0):
     """bjxa_hip_decode_async; `events` = optional hipEvent_t pair recorded
     around the speculative-decode kernel on `stream`."""
     s = HipStream(d_src, d_dst, frames, eblocks, bits, channels, (ctypes.c_int16 * 4)(*state))
-    t = HipTuning(chunk, warmup, (ctypes.c_void_p * 2)(*events))
+    t = HipTuning(chunk, warmup, (ctypes.c_void_p * 2)(*events), variant)
     _check(lib().bjxa_hip_decode_async(ctypes.byref(s), d_ws, ws_len, d_status,
                                        ctypes.byref(t), stream), "bjxa_hip_decode_async")
 

@@ -51,8 +51,27 @@ xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
     int32_t &p1)
 {
 	int32_t t = top >> sh;
+#ifdef XA_STEP_SHORT
+	/*
+	 * Shorter dependency chain: t*256 + p1*K1 is ready one step early
+	 * (p1 is the previous step's p0), so g2 = p0*K0 + that runs beside
+	 * g = p0*K0 + p1*K1, and floor((g2 + bias) / 256) = t + trunc(g/256)
+	 * because t*256 is a multiple of 256.  Chain: mad, ashr, add, ashr,
+	 * med3 (5 instead of 6).  The empty asm keeps the compiler from
+	 * re-deriving g2 as g + t*256 on the chain.
+	 */
+	int32_t c1 = __mul24(p1, k1);
+	int32_t c2 = c1 + (t << 8);
+	int32_t k0b = k0;
+	asm("" : "+v"(k0b), "+v"(c1), "+v"(c2));
+	int32_t g = __mul24(p0, k0) + c1;
+	int32_t g2 = __mul24(p0, k0b) + c2;
+	asm("" : "+v"(g2));
+	int32_t s = (g2 + (int32_t)((uint32_t)(g >> 31) >> 24)) >> 8;
+#else
 	int32_t g = __mul24(p0, k0) + __mul24(p1, k1);
 	int32_t s = t + ((g + (int32_t)((uint32_t)(g >> 31) >> 24)) >> 8);
+#endif
 	s = min(max(s, -32768), 32767);
 	p1 = p0;
 	p0 = s;
@@ -69,7 +88,7 @@ xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
 __device__ __forceinline__ uint32_t
 xa_byte_top(const uint32_t *w, const int b)
 {
-	return __builtin_amdgcn_perm(0u, w[b >> 2], 0x0c0c0c0cu |
+	return __builtin_amdgcn_perm(0u, w[b >> 2], 0x000c0c0cu |
 	    ((uint32_t)(b & 3) << 24));
 }
 
@@ -78,14 +97,14 @@ __device__ __forceinline__ uint32_t
 xa_2bytes_top(const uint32_t *w, const int b)
 {
 	if ((b >> 2) == ((b + 1) >> 2)) {
-		return __builtin_amdgcn_perm(0u, w[b >> 2], 0x0c0c0000u |
+		return __builtin_amdgcn_perm(0u, w[b >> 2], 0x00000c0cu |
 		    ((uint32_t)(b & 3) << 24) | ((uint32_t)((b + 1) & 3) << 16));
 	}
 	/* b is byte 3 of w[i], b+1 is byte 0 of w[i+1]; v_perm_b32 indexes
 	 * the 64-bit {S0, S1}: selectors 0-3 pick bytes of S1 (w[i]),
 	 * 4-7 bytes of S0 (w[i+1]) */
 	return __builtin_amdgcn_perm(w[(b + 1) >> 2], w[b >> 2],
-	    0x0c0c0000u | (3u << 24) | (4u << 16));
+	    0x00000c0cu | (3u << 24) | (4u << 16));
 }
 
 /*

@@ -37,7 +37,7 @@ struct xa_dec_args {
 };
 
 hipError_t xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
-    hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+    unsigned variant, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 
 struct xa_enc_args {
 	const uint8_t *src;	/* PCM frames, 16-bit, channels interleaved */

@@ -54,7 +54,7 @@ pick_tuning(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 static size_t
 ws_bytes(uint32_t nchunks)
 {
-	return XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 4) + 64;
+	return XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 8) + 64;	/* g, e, queue (2x: the tail heap may hold duplicates) */
 }
 
 extern "C" size_t
@@ -137,7 +137,8 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.e = a.g + a.nchunks;
 	a.queue = (uint32_t *)(a.e + a.nchunks);
 	a.status = d_status;
-	if (xa_decode_launch(a, s->bits, s->channels, (hipStream_t)stream,
+	if (xa_decode_launch(a, s->bits, s->channels, tune ? tune->variant : 0,
+	    (hipStream_t)stream,
 	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
 	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
 		errno = EIO;

@@ -45,6 +45,7 @@ typedef struct {
 	int32_t		warmup;		/* speculative warm-up eblocks, -1 = auto */
 	void		*ev_spec[2];	/* hipEvent_t pair recorded on `stream`
 					 * around the speculative-decode kernel */
+	uint32_t	variant;	/* kernel structure; 0 = default */
 } bjxa_hip_tuning_t;
 
 /*
