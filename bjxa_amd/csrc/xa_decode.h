@@ -11,6 +11,7 @@
 #define XA_CTL_ERR	0	/* min channel-block index with gain >= 5 */
 #define XA_CTL_NQ	1	/* re-check queue length */
 #define XA_CTL_FIXED	2	/* chunks repaired by K2 */
+#define XA_CTL_TICKET	3	/* K2 workgroups finished (last one runs the tail) */
 #define XA_CTL_WORDS	64	/* 256 B */
 
 /* status words written by the tail kernel */

@@ -23,7 +23,8 @@
  *                     block until its block-end state meets the stored
  *                     trajectory (everything after is then unchanged).  A
  *                     chunk that never meets it rewrites e[q] and queues q+1.
- *  K3 xa_decode_tail  one thread drains that queue in chunk order, so a
+ *                     The last workgroup to finish (arrival ticket) drains
+ *                     that queue in chunk order with one thread, so a
  *                     cascade through several chunks is repaired exactly.
  *
  * By induction from chunk 0 every chunk ends up decoded from its true start
@@ -213,7 +214,7 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
  * grid's last wave only) per-piece bounds and a 2-byte tail for the
  * stream's cut last block.
  */
-template <int LB>
+template <int LB, bool NT>
 __device__ __forceinline__ void
 store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
     uint32_t wchunk0, uint32_t chunk_bytes, uint32_t rel_off, bool wave_full,
@@ -224,9 +225,14 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 		uint8_t *gp = gbase + rel_off;
 		const uint64_t istride = (uint64_t)LPI * chunk_bytes;
 #pragma unroll
-		for (int i = 0; i < P; i++)
-			*(u32x4a *)(gp + i * istride) =
-			    *(const u32x4a *)(lbase + i * LPI * LINE);
+		for (int i = 0; i < P; i++) {
+			const u32x4a v = *(const u32x4a *)(lbase + i * LPI * LINE);
+			if (NT)
+				__builtin_nontemporal_store(v,
+				    (u32x4a *)(gp + i * istride));
+			else
+				*(u32x4a *)(gp + i * istride) = v;
+		}
 		return;
 	}
 	/* launder the inputs so none of this rare path's address arithmetic
@@ -306,7 +312,7 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, uint32_t wchunk0,
  *  LB     output line bytes per lane per store phase (64, or the eblock's
  *         64*ch).
  */
-template <int BITS, int CH, bool SPLIT, int LB>
+template <int BITS, int CH, bool SPLIT, int LB, bool NT>
 __global__ __launch_bounds__(64 * XA_SPEC_WPB) void
 xa_decode_spec(xa_dec_args a)
 {
@@ -409,7 +415,7 @@ xa_decode_spec(xa_dec_args a)
 			const int64_t b = b0 + s;
 			auto flush = [&](int h) {
 				wave_lds_sync();
-				store_lines<LB>(a, obuf, lane, wchunk0, chunk_bytes,
+				store_lines<LB, NT>(a, obuf, lane, wchunk0, chunk_bytes,
 				    (uint32_t)s * OB + (uint32_t)LB * h, wave_full, gbase,
 				    lbase);
 				wave_lds_sync();
@@ -571,34 +577,6 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s)
 	return false;
 }
 
-/* K2.  One thread per chunk; only mismatching chunks do work. */
-template <int BITS, int CH>
-__global__ __launch_bounds__(256) void
-xa_decode_fix(xa_dec_args a)
-{
-	const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-	if (q == 0 || q >= a.nchunks)
-		return;
-	/* e[q-1] may be rewritten concurrently by chunk q-1's fixer; whichever
-	 * value is read is recorded in g[q], and that fixer queues q for the
-	 * tail pass, which re-checks it */
-	const uint64_t s64 = __hip_atomic_load((const uint64_t *)&a.e[q - 1],
-	    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-	const uint64_t g64 = *(const uint64_t *)&a.g[q];
-	if (s64 == g64)
-		return;
-	uint2 s;
-	s.x = (uint32_t)s64;
-	s.y = (uint32_t)(s64 >> 32);
-	atomicAdd(&a.ctl[XA_CTL_FIXED], 1u);
-	const bool met = fix_chunk<BITS, CH>(a, q, s);
-	a.g[q] = s;
-	if (!met && q + 1 < a.nchunks) {
-		uint32_t i = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
-		a.queue[i] = q + 1;
-	}
-}
-
 /* binary min-heap over queue[0..n) (single thread) */
 __device__ static void
 heap_push(uint32_t *h, uint32_t &n, uint32_t v)
@@ -636,15 +614,14 @@ heap_pop(uint32_t *h, uint32_t &n)
 }
 
 /*
- * K3.  A single thread drains the re-check queue in chunk order (a heap,
- * so even a pathological cascade costs O(n log n) bookkeeping).
+ * The sequential tail (one thread): drain the re-check queue in chunk order
+ * (a heap, so even a pathological cascade costs O(n log n) bookkeeping),
+ * then publish the status words and reset the control words.
  */
 template <int BITS, int CH>
-__global__ __launch_bounds__(64) void
-xa_decode_tail(xa_dec_args a)
+__device__ void
+drain_tail(const xa_dec_args &a)
 {
-	if (threadIdx.x != 0)
-		return;
 	const uint32_t nq = a.ctl[XA_CTL_NQ];
 	uint32_t n = 0, tail = 0;
 	for (uint32_t i = 0; i < nq; i++)
@@ -670,6 +647,60 @@ xa_decode_tail(xa_dec_args a)
 	a.ctl[XA_CTL_ERR] = 0xffffffffu;
 	a.ctl[XA_CTL_NQ] = 0;
 	a.ctl[XA_CTL_FIXED] = 0;
+	a.ctl[XA_CTL_TICKET] = 0;
+}
+
+/*
+ * K2.  Verify every chunk boundary (grid-stride) and repair mismatching
+ * chunks in parallel; the last workgroup to finish then runs the
+ * sequential tail, so the whole repair is one launch.
+ */
+template <int BITS, int CH>
+__global__ __launch_bounds__(256) void
+xa_decode_fix(xa_dec_args a)
+{
+	__shared__ uint32_t last;
+	const uint32_t stride = gridDim.x * 256u;
+	for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < a.nchunks;
+	    q += stride) {
+		if (q == 0)
+			continue;
+		/* e[q-1] may be rewritten concurrently by chunk q-1's fixer;
+		 * whichever value is read is recorded in g[q], and that fixer
+		 * queues q for the tail, which re-checks it */
+		const uint64_t s64 = __hip_atomic_load(
+		    (const uint64_t *)&a.e[q - 1], __ATOMIC_RELAXED,
+		    __HIP_MEMORY_SCOPE_AGENT);
+		const uint64_t g64 = *(const uint64_t *)&a.g[q];
+		if (s64 == g64)
+			continue;
+		uint2 s;
+		s.x = (uint32_t)s64;
+		s.y = (uint32_t)(s64 >> 32);
+		atomicAdd(&a.ctl[XA_CTL_FIXED], 1u);
+		const bool met = fix_chunk<BITS, CH>(a, q, s);
+		a.g[q] = s;
+		if (!met && q + 1 < a.nchunks) {
+			uint32_t i = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
+			a.queue[i] = q + 1;
+		}
+	}
+	/* arrival ticket (release: every wave's stores done at the barrier,
+	 * then lane 0's agent fence; MI355X_MICROARCH.md inter-workgroup
+	 * visibility recipe) */
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		__threadfence();
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		last = atomicAdd(&a.ctl[XA_CTL_TICKET], 1u) == gridDim.x - 1;
+	}
+	__syncthreads();
+	if (!last || threadIdx.x != 0)
+		return;
+	/* acquire: this CU now sees every other workgroup's writes */
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	drain_tail<BITS, CH>(a);
 }
 
 /* ------------------------------------------------------------------ */
@@ -681,25 +712,27 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 {
 	const unsigned per = 64u * XA_SPEC_WPB;
 	const unsigned grid = (a.nchunks + per - 1) / per;
-	const unsigned grid2 = (a.nchunks + 255u) / 256u;
+	unsigned grid2 = (a.nchunks + 255u) / 256u;
+	if (grid2 > 512u)
+		grid2 = 512u;
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
-	/* variant bit 0: SPLIT; bit 1: 64-B lines (else whole eblocks) */
+	/* variant bit 0: SPLIT regions; bit 1: non-temporal output stores */
 	switch (variant & 3u) {
 	case 0:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, 64 * CH>),
+		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, 64 * CH, false>),
 		    dim3(grid), dim3(per), 0, st, a);
 		break;
 	case 1:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, true, 64 * CH>),
+		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, true, 64 * CH, false>),
 		    dim3(grid), dim3(per), 0, st, a);
 		break;
 	case 2:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, 64>),
+		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, 64 * CH, true>),
 		    dim3(grid), dim3(per), 0, st, a);
 		break;
 	default:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, true, 64>),
+		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, true, 64 * CH, true>),
 		    dim3(grid), dim3(per), 0, st, a);
 		break;
 	}
@@ -707,8 +740,6 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 		(void)hipEventRecord(ev1, st);
 	hipLaunchKernelGGL((xa_decode_fix<BITS, CH>), dim3(grid2), dim3(256), 0,
 	    st, a);
-	hipLaunchKernelGGL((xa_decode_tail<BITS, CH>), dim3(1), dim3(64), 0, st,
-	    a);
 	return hipGetLastError();
 }
 

@@ -16,7 +16,14 @@
 #include "../../include/bjxa_hip.h"
 
 #define DEFAULT_WARMUP	8u	/* eblocks; SURVEY App. C / DESIGN.md */
-#define TARGET_LANES	(256u * 12u * 64u)
+/*
+ * Automatic chunk length: aim for about 2 (stereo) or 4 (mono) resident
+ * 256-lane workgroups per CU on the 256 CUs -- the speculative kernel is
+ * throughput-bound per CU, so its time goes as (workgroups on the busiest
+ * CU) x (chunk + warm-up); see DESIGN.md "Tuning".
+ */
+#define TARGET_LANES_STEREO	(256u * 2u * 256u)
+#define TARGET_LANES_MONO	(256u * 4u * 256u)
 
 static int
 gpu_present(void)
@@ -43,12 +50,24 @@ pick_tuning(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 	uint32_t c = t && t->chunk ? t->chunk : 0;
 	uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup : DEFAULT_WARMUP;
 	if (c == 0) {
-		c = (eblocks + TARGET_LANES - 1) / TARGET_LANES;
+		const uint32_t lanes = ch == 2 ? TARGET_LANES_STEREO :
+		    TARGET_LANES_MONO;
+		c = (eblocks + lanes - 1) / lanes;
 		if (c < 16)
 			c = 16;
 	}
 	*C = round_up(c, G);
 	*W = round_up(w, G);
+}
+
+/* kernel structure: bit 1 = non-temporal PCM stores (measured: a small
+ * gain for stereo, a loss for mono) */
+static unsigned
+pick_variant(unsigned ch, const bjxa_hip_tuning_t *t)
+{
+	if (t && t->variant)
+		return t->variant & 0xffu;
+	return ch == 2 ? 2u : 0u;
 }
 
 static size_t
@@ -137,7 +156,7 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.e = a.g + a.nchunks;
 	a.queue = (uint32_t *)(a.e + a.nchunks);
 	a.status = d_status;
-	if (xa_decode_launch(a, s->bits, s->channels, tune ? tune->variant : 0,
+	if (xa_decode_launch(a, s->bits, s->channels, pick_variant(s->channels, tune),
 	    (hipStream_t)stream,
 	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
 	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
