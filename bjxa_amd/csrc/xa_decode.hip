@@ -51,6 +51,9 @@
 #ifndef XA_SPEC_WPB
 #define XA_SPEC_WPB 4		/* waves per workgroup */
 #endif
+#ifndef XA_DMA_AUX
+#define XA_DMA_AUX 0		/* cache policy bits of the input LDS-DMA */
+#endif
 
 /* ------------------------------------------------------------------ */
 
@@ -283,7 +286,7 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, uint32_t wchunk0,
 		for (int i = 0; i < GDW; i++)
 			__builtin_amdgcn_global_load_lds(
 			    (const void *)(base + voff[i]), LDS_PTR(ibuf + i * 256),
-			    4, 0, 0);
+			    4, 0, XA_DMA_AUX);
 		return;
 	}
 	/* rare path (the grid's first and last waves): launder the inputs so
@@ -299,7 +302,7 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, uint32_t wchunk0,
 		int64_t byte = ((int64_t)(wc + seg) * C + r) * g::EBSZ + off * 4;
 		byte = byte < 0 ? 0 : (byte > last ? last : byte);
 		__builtin_amdgcn_global_load_lds((const void *)(src + byte),
-		    LDS_PTR(ibuf + i * 256), 4, 0, 0);
+		    LDS_PTR(ibuf + i * 256), 4, 0, XA_DMA_AUX);
 	}
 }
 
@@ -467,11 +470,11 @@ xa_decode_spec(xa_dec_args a)
  * decoder (one thread; stores go straight to global memory).  Stops once a
  * block-end state equals the stored trajectory's (nothing after it can
  * change).  Returns true if it met the stored trajectory; otherwise stores
- * the new end state in e[q].
+ * the new end state in e[q] and returns it in `exit`.
  */
 template <int BITS, int CH>
 __device__ bool
-fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s)
+fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 {
 	typedef geo<BITS, CH> g;
 	constexpr int G = g::G, OB = g::OB, WD = g::WD;
@@ -490,31 +493,36 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s)
 	 * Latency is what matters here (one busy lane per wave), so no load
 	 * sits under a divergent branch -- hipcc drains vmcnt(0) right after
 	 * such loads.  Every load is issued unconditionally with clamped
-	 * indices (results past the chunk are never used), the decode lands in
-	 * registers, and only the stores are predicated.
+	 * indices (results past the chunk are never used), one group ahead:
+	 * the next eblock's window and the next group's old block-end states.
+	 * The decode lands in registers; only the stores are predicated.
 	 */
 	const int64_t ndw = (eblocks * g::EBSZ + 3) / 4;	/* source dwords */
 	uint32_t buf[2][WD];
-	bool met = false;
-	load_window<BITS, CH, 0>(buf[0], a.src, b0);
-	for (int64_t bg = b0; bg < b1; bg += G) {
-		/* old trajectory's block-end states (frames 30, 31), read before
-		 * any rewrite; only used where b + 1 < eblocks */
-		uint32_t old[G][CH];
-		auto rd = [&](auto uc) {
+	/* old trajectory's block-end states (frames 30, 31) of a group, read
+	 * before any rewrite; only used where b + 1 < eblocks */
+	uint32_t old[G][CH], nxt[G][CH];
+	auto rd = [&](uint32_t (*o_)[CH], int64_t bg) {
+		auto one = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
 			const int64_t b = min(bg + u, eblocks - 1);
 			const uint8_t *o = a.dst + b * OB;
 			if (CH == 2) {
 				uint2 f = *(const uint2 *)(o + 30 * 4);
-				old[u][0] = (f.y & 0xffffu) | (f.x << 16);
-				old[u][CH - 1] = (f.y >> 16) | (f.x & 0xffff0000u);
+				o_[u][0] = (f.y & 0xffffu) | (f.x << 16);
+				o_[u][CH - 1] = (f.y >> 16) | (f.x & 0xffff0000u);
 			} else {
 				uint32_t f = *(const uint32_t *)(o + 30 * 2);
-				old[u][0] = (f >> 16) | (f << 16);
+				o_[u][0] = (f >> 16) | (f << 16);
 			}
 		};
-		sfor<0, G>::run(rd);
+		sfor<0, G>::run(one);
+	};
+	bool met = false;
+	load_window<BITS, CH, 0>(buf[0], a.src, b0);
+	rd(old, b0);
+	for (int64_t bg = b0; bg < b1; bg += G) {
+		rd(nxt, bg + G);
 		auto body = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
 			const int64_t b = bg + u;
@@ -567,13 +575,17 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s)
 		sfor<0, G>::run(body);
 		if (met)
 			break;
+#pragma unroll
+		for (int u = 0; u < G; u++)
+#pragma unroll
+			for (int c = 0; c < CH; c++)
+				old[u][c] = nxt[u][c];
 	}
 	if (met)
 		return true;
-	uint2 ev;
-	ev.x = xa_pack_state(p0[0], p1[0]);
-	ev.y = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
-	a.e[q] = ev;
+	exit.x = xa_pack_state(p0[0], p1[0]);
+	exit.y = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
+	a.e[q] = exit;
 	return false;
 }
 
@@ -632,7 +644,8 @@ drain_tail(const xa_dec_args &a)
 		if (s.x == gq.x && s.y == gq.y)
 			continue;
 		tail++;
-		const bool met = fix_chunk<BITS, CH>(a, q, s);
+		uint2 ex;
+		const bool met = fix_chunk<BITS, CH>(a, q, s, ex);
 		a.g[q] = s;
 		if (!met && q + 1 < a.nchunks)
 			heap_push(a.queue, n, q + 1);
@@ -651,47 +664,88 @@ drain_tail(const xa_dec_args &a)
 }
 
 /*
- * K2.  Verify every chunk boundary (grid-stride) and repair mismatching
- * chunks in parallel; the last workgroup to finish then runs the
- * sequential tail, so the whole repair is one launch.
+ * K2.  Verify every chunk boundary and repair mismatching chunks in
+ * parallel; the last workgroup to finish then runs the sequential tail, so
+ * the whole repair is one launch.  Per pass a workgroup checks
+ * 256 * XA_FIX_CPT consecutive boundaries (a thread reads XA_FIX_CPT
+ * consecutive e/g pairs), lists the mismatches in LDS, and then gives each
+ * listed chunk a thread of its own: repairs of one wave run side by side,
+ * so the pass costs the longest repair, not their sum.  Few, fat workgroups
+ * keep the arrival ticket (one contended word) and the release fences
+ * (only in workgroups that wrote) cheap.
  */
+#ifndef XA_FIX_CPT
+#define XA_FIX_CPT 4
+#endif
+
 template <int BITS, int CH>
 __global__ __launch_bounds__(256) void
 xa_decode_fix(xa_dec_args a)
 {
-	__shared__ uint32_t last;
-	const uint32_t stride = gridDim.x * 256u;
-	for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < a.nchunks;
-	    q += stride) {
-		if (q == 0)
-			continue;
+	constexpr uint32_t SPAN = 256u * XA_FIX_CPT;
+	__shared__ uint32_t last, nfix;
+	__shared__ uint32_t fixq[SPAN];
+	__shared__ uint2 fixs[SPAN];
+	const uint32_t n = a.nchunks;
+	const uint64_t *e64 = (const uint64_t *)a.e;
+	const uint64_t *g64 = (const uint64_t *)a.g;
+	bool wrote = false;
+	for (uint32_t base = blockIdx.x * SPAN; base < n;
+	    base += gridDim.x * SPAN) {
+		if (threadIdx.x == 0)
+			nfix = 0;
+		__syncthreads();
 		/* e[q-1] may be rewritten concurrently by chunk q-1's fixer;
 		 * whichever value is read is recorded in g[q], and that fixer
 		 * queues q for the tail, which re-checks it */
-		const uint64_t s64 = __hip_atomic_load(
-		    (const uint64_t *)&a.e[q - 1], __ATOMIC_RELAXED,
-		    __HIP_MEMORY_SCOPE_AGENT);
-		const uint64_t g64 = *(const uint64_t *)&a.g[q];
-		if (s64 == g64)
-			continue;
-		uint2 s;
-		s.x = (uint32_t)s64;
-		s.y = (uint32_t)(s64 >> 32);
-		atomicAdd(&a.ctl[XA_CTL_FIXED], 1u);
-		const bool met = fix_chunk<BITS, CH>(a, q, s);
-		a.g[q] = s;
-		if (!met && q + 1 < a.nchunks) {
-			uint32_t i = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
-			a.queue[i] = q + 1;
+		const uint32_t t0 = base + threadIdx.x * XA_FIX_CPT;
+		uint64_t ev[XA_FIX_CPT], gv[XA_FIX_CPT];
+#pragma unroll
+		for (int i = 0; i < XA_FIX_CPT; i++) {
+			const uint32_t q = min(t0 + i, n - 1);
+			ev[i] = __hip_atomic_load(&e64[q > 0 ? q - 1 : 0],
+			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			gv[i] = g64[q];
 		}
+#pragma unroll
+		for (int i = 0; i < XA_FIX_CPT; i++) {
+			const uint32_t q = t0 + i;
+			if (q > 0 && q < n && ev[i] != gv[i]) {
+				const uint32_t k = atomicAdd(&nfix, 1u);
+				fixq[k] = q;
+				fixs[k] = make_uint2((uint32_t)ev[i],
+				    (uint32_t)(ev[i] >> 32));
+			}
+		}
+		__syncthreads();
+		const uint32_t nf = nfix;
+		for (uint32_t k = threadIdx.x; k < nf; k += 256u) {
+			const uint32_t q = fixq[k];
+			const uint2 s = fixs[k];
+			uint2 ex;
+			const bool met = fix_chunk<BITS, CH>(a, q, s, ex);
+			a.g[q] = s;
+			wrote = true;
+			if (!met && q + 1 < n) {
+				uint32_t i = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
+				a.queue[i] = q + 1;
+			}
+		}
+		if (threadIdx.x == 0 && nf)
+			atomicAdd(&a.ctl[XA_CTL_FIXED], nf);
+		__syncthreads();
 	}
-	/* arrival ticket (release: every wave's stores done at the barrier,
-	 * then lane 0's agent fence; MI355X_MICROARCH.md inter-workgroup
-	 * visibility recipe) */
-	__syncthreads();
+	/* arrival ticket.  Release (MI355X_MICROARCH.md inter-workgroup
+	 * recipe): every wave's stores done at the barrier, then lane 0's
+	 * agent fence and its wait, then the ticket -- skipped by workgroups
+	 * that stored nothing */
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	const int any = __syncthreads_or(wrote);
 	if (threadIdx.x == 0) {
-		__threadfence();
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		if (any) {
+			__threadfence();
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
 		last = atomicAdd(&a.ctl[XA_CTL_TICKET], 1u) == gridDim.x - 1;
 	}
 	__syncthreads();
@@ -712,9 +766,9 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 {
 	const unsigned per = 64u * XA_SPEC_WPB;
 	const unsigned grid = (a.nchunks + per - 1) / per;
-	unsigned grid2 = (a.nchunks + 255u) / 256u;
-	if (grid2 > 512u)
-		grid2 = 512u;
+	unsigned grid2 = (a.nchunks + 256u * XA_FIX_CPT - 1) / (256u * XA_FIX_CPT);
+	if (grid2 > 256u)
+		grid2 = 256u;
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
 	/* variant bit 0: SPLIT regions; bit 1: non-temporal output stores */
