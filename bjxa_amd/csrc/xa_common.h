@@ -51,6 +51,14 @@ xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
     int32_t &p1)
 {
 	int32_t t = top >> sh;
+#if defined(XA_DBG_STEP)
+	/* diagnostic build only (wrong output): no predictor */
+	(void)k0;
+	(void)k1;
+	p1 = p0;
+	p0 = t;
+	return t;
+#endif
 #ifdef XA_STEP_SHORT
 	/*
 	 * Shorter dependency chain: t*256 + p1*K1 is ready one step early

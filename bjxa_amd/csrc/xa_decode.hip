@@ -35,9 +35,9 @@
  * mono eblocks) = 4*(bits*4+1) bytes, a whole number of dwords.  Each wave
  * owns two LDS regions:
  *  - input: the group of each of its 64 chunks, fetched by LDS-DMA with the
- *    64 segments concatenated so every DMA instruction reads ~256 contiguous
- *    bytes (instead of 64 scattered 16-B pieces, which saturated the texture
- *    addresser).  A lane copies its segment to VGPRs and the next group's
+ *    64 segments concatenated so every DMA instruction reads 64 x 4/12/16
+ *    contiguous bytes (instead of 64 scattered 16-B pieces, which saturated
+ *    the texture addresser).  A lane copies its segment to VGPRs and the next group's
  *    DMA is issued at once, overlapping the decode.
  *  - output: one 64-B line per lane (a mono block, or half a stereo eblock),
  *    written back so each store instruction covers 16 whole 64-B lines.
@@ -92,58 +92,19 @@ template <int BITS, int CH> struct geo {
 	static constexpr int G = 4 / CH;		/* eblocks per group */
 	static constexpr int GDW = BSZ;			/* dwords per group */
 	static constexpr int OB = 64 * CH;		/* PCM bytes per eblock */
-	/* window of eblock u (0..G-1) of a group: first dword, byte offset */
-	static constexpr int wbase(int u) { return (u * EBSZ) >> 2; }
-	static constexpr int woff(int u) { return (u * EBSZ) & 3; }
-	static constexpr int wlen(int u) { return (woff(u) + EBSZ + 3) >> 2; }
-	static constexpr int wmax() {
-		int m = 0;
-		for (int u = 0; u < G; u++)
-			m = wlen(u) > m ? wlen(u) : m;
-		return m;
-	}
-	static constexpr int WD = wmax();
+	/* LDS-DMA: 16-B pieces (packed lane-linear in LDS at any 4-B aligned
+	 * source; 12-B pieces are not: they land at a 16-B lane stride), so a
+	 * group's segment is read rounded up to SEGB bytes -- the extra bytes
+	 * are the start of the chunk's next group -- and segments sit SEGB
+	 * apart in LDS (8-bit: 144 B = 36 dwords, 16 lanes of a ds_read_b128
+	 * phase hit all 64 banks once) */
+#ifndef XA_DMA_MAXPIECE
+#define XA_DMA_MAXPIECE 16
+#endif
+	static constexpr int PS = XA_DMA_MAXPIECE >= 16 ? 16 : 4;
+	static constexpr int SEGB = (GDW * 4 + PS - 1) / PS * PS;
+	static constexpr int NP = SEGB / PS;		/* pieces per segment */
 };
-
-/*
- * Load the window of eblock b (b % G == U) into w (repair path).  Whole
- * dwords only; the dword holding the stream's last byte is read whole,
- * nothing past it.
- */
-template <int BITS, int CH, int U>
-__device__ __forceinline__ void
-load_window(uint32_t *w, const uint8_t *src, int64_t b)
-{
-	typedef geo<BITS, CH> g;
-	constexpr int N = g::wlen(U);
-	const uint32_t *p = (const uint32_t *)(src + (size_t)(b - U) * g::EBSZ) +
-	    g::wbase(U);
-#pragma unroll
-	for (int i = 0; i < N / 4; i++) {
-		u32x4 v = ((const u32x4 *)p)[i];
-		w[4 * i + 0] = v.x;
-		w[4 * i + 1] = v.y;
-		w[4 * i + 2] = v.z;
-		w[4 * i + 3] = v.w;
-	}
-#pragma unroll
-	for (int i = (N / 4) * 4; i < N; i++)
-		w[i] = p[i];
-}
-
-/* load_window with every dword index clamped into the stream (no branch) */
-template <int BITS, int CH, int U>
-__device__ __forceinline__ void
-load_window_clamped(uint32_t *w, const uint8_t *src, int64_t b, int64_t ndw)
-{
-	typedef geo<BITS, CH> g;
-	constexpr int N = g::wlen(U);
-	const int64_t d0 = (b - U) * g::EBSZ / 4 + g::wbase(U);
-	const uint32_t *p = (const uint32_t *)src;
-#pragma unroll
-	for (int i = 0; i < N; i++)
-		w[i] = p[min(d0 + i, ndw - 1)];
-}
 
 /*
  * Decode the channel blocks of one eblock whose first byte is byte O of w,
@@ -224,6 +185,11 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
     uint8_t *gbase, const uint8_t *lbase)
 {
 	constexpr int LINE = LB + 16, P = LB / 16, LPI = 64 / P;
+#ifdef XA_DBG_NOSTORE
+	/* diagnostic build only (no output) */
+	if (wave_full)
+		return;
+#endif
 	if (wave_full) {
 		uint8_t *gp = gbase + rel_off;
 		const uint64_t istride = (uint64_t)LPI * chunk_bytes;
@@ -263,13 +229,34 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 	}
 }
 
+/* one LDS-DMA instruction of PS bytes per lane (the builtin wants a
+ * literal size) */
+template <int PS> __device__ __forceinline__ void dma(const void *, uint8_t *);
+template <> __device__ __forceinline__ void
+dma<4>(const void *g, uint8_t *l)
+{
+	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 4, 0, XA_DMA_AUX);
+}
+template <> __device__ __forceinline__ void
+dma<12>(const void *g, uint8_t *l)
+{
+	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 12, 0, XA_DMA_AUX);
+}
+template <> __device__ __forceinline__ void
+dma<16>(const void *g, uint8_t *l)
+{
+	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 16, 0, XA_DMA_AUX);
+}
+
 /*
  * Stage one group of each of the wave's 64 chunks into `ibuf` by LDS-DMA:
- * the 64 segments are concatenated and instruction i moves dwords
- * [64i, 64i+64) of that concatenation (lane t: dword 64i+t).  `rel` is the
- * group's first eblock relative to each chunk's start.  Segments outside
- * the stream (warm-up before eblock 0, the ragged end) are clamped onto
- * valid dwords; their lanes never decode them.
+ * the 64 segments (SEGB bytes each) are concatenated and cut into PS-byte
+ * pieces; instruction i moves pieces [64i, 64i+64) of that concatenation
+ * (lane t: piece 64i+t), i.e. 64*PS contiguous bytes of one or two
+ * segments.
+ * `rel` is the group's first eblock relative to each chunk's start.
+ * Segments outside the stream (warm-up before eblock 0, the ragged end) are
+ * clamped onto valid bytes; their lanes never decode them.
  */
 template <int BITS, int CH>
 __device__ __forceinline__ void
@@ -277,32 +264,35 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, uint32_t wchunk0,
     int64_t rel, const uint32_t *voff)
 {
 	typedef geo<BITS, CH> g;
-	constexpr int GDW = g::GDW;
+	constexpr int NP = g::NP, PS = g::PS;
 	const int64_t e_first = (int64_t)wchunk0 * a.C + rel;
 	const int64_t e_end = (int64_t)(wchunk0 + 63u) * a.C + rel + g::G;
-	if (e_first >= 0 && e_end <= (int64_t)a.eblocks) {
+	/* the last segment's read may run SEGB - 4*GDW bytes past its group */
+	if (e_first >= 0 && e_end * g::EBSZ + (g::SEGB - 4 * g::GDW) <=
+	    (int64_t)a.eblocks * g::EBSZ) {
 		const uint8_t *base = a.src + (size_t)e_first * g::EBSZ;
 #pragma unroll
-		for (int i = 0; i < GDW; i++)
-			__builtin_amdgcn_global_load_lds(
-			    (const void *)(base + voff[i]), LDS_PTR(ibuf + i * 256),
-			    4, 0, XA_DMA_AUX);
+		for (int i = 0; i < NP; i++)
+			dma<PS>(base + voff[i], ibuf + i * 64 * PS);
 		return;
 	}
-	/* rare path (the grid's first and last waves): launder the inputs so
-	 * none of its arithmetic is hoisted into the caller's loops */
+	/* rare path (the grid's first and last waves): dword pieces into the
+	 * same SEGB-strided layout, each clamped into the stream whole (the
+	 * dword holding the stream's last byte is read whole, nothing past
+	 * it).  Launder the inputs so none of its arithmetic is hoisted into
+	 * the caller's loops. */
 	uint32_t wc = wchunk0, C = a.C, neb = a.eblocks;
 	int64_t r = rel;
 	const uint8_t *src = a.src;
 	asm volatile("" : "+v"(wc), "+v"(C), "+v"(neb), "+v"(r), "+v"(src));
+	constexpr int SD = g::SEGB / 4;
 	const int64_t last = ((int64_t)neb * g::EBSZ - 1) & ~(int64_t)3;
 #pragma nounroll
-	for (int i = 0; i < GDW; i++) {
-		const int k = i * 64 + lane, seg = k / GDW, off = k % GDW;
+	for (int i = 0; i < SD; i++) {
+		const int k = i * 64 + lane, seg = k / SD, off = k % SD;
 		int64_t byte = ((int64_t)(wc + seg) * C + r) * g::EBSZ + off * 4;
 		byte = byte < 0 ? 0 : (byte > last ? last : byte);
-		__builtin_amdgcn_global_load_lds((const void *)(src + byte),
-		    LDS_PTR(ibuf + i * 256), 4, 0, XA_DMA_AUX);
+		dma<4>(src + byte, ibuf + i * 256);
 	}
 }
 
@@ -321,7 +311,7 @@ xa_decode_spec(xa_dec_args a)
 {
 	typedef geo<BITS, CH> g;
 	constexpr int G = g::G, OB = g::OB, EBSZ = g::EBSZ, GDW = g::GDW;
-	constexpr int IBUF = 64 * GDW * 4;	/* input stage, per wave */
+	constexpr int IBUF = 64 * g::SEGB;	/* input stage, per wave */
 	constexpr int LINE = LB + 16;		/* output line + pad */
 	constexpr int OBUF = 64 * LINE;		/* output stage, per wave */
 	constexpr int REGION = SPLIT ? IBUF + OBUF : (IBUF > OBUF ? IBUF : OBUF);
@@ -344,12 +334,13 @@ xa_decode_spec(xa_dec_args a)
 	const int W = (int)a.W;
 
 	/* DMA source offsets (bytes from the wave's segment 0) of this lane's
-	 * dword in each stage instruction; the same for every group */
-	uint32_t voff[GDW];
+	 * piece in each stage instruction; the same for every group */
+	constexpr int NP = g::NP, PS = g::PS;
+	uint32_t voff[NP];
 #pragma unroll
-	for (int i = 0; i < GDW; i++) {
+	for (int i = 0; i < NP; i++) {
 		const int k = i * 64 + lane;
-		voff[i] = (uint32_t)(k / GDW) * a.C * EBSZ + (uint32_t)(k % GDW) * 4u;
+		voff[i] = (uint32_t)(k / NP) * a.C * EBSZ + (uint32_t)(k % NP) * PS;
 	}
 
 	int32_t p0[CH], p1[CH];
@@ -362,7 +353,7 @@ xa_decode_spec(xa_dec_args a)
 	}
 
 	uint32_t w[GDW];
-	const uint32_t *mine = (const uint32_t *)(ibuf + lane * GDW * 4);
+	const uint32_t *mine = (const uint32_t *)(ibuf + lane * g::SEGB);
 	auto none = [](int) {};
 	stage_group<BITS, CH>(a, ibuf, lane, wchunk0, -W, voff);
 
@@ -466,126 +457,204 @@ xa_decode_spec(xa_dec_args a)
 /* repair path                                                          */
 
 /*
- * Re-decode chunk q from state `s`, rewriting its PCM, with the same block
- * decoder (one thread; stores go straight to global memory).  Stops once a
- * block-end state equals the stored trajectory's (nothing after it can
- * change).  Returns true if it met the stored trajectory; otherwise stores
- * the new end state in e[q] and returns it in `exit`.
+ * The repair path is latency-bound (a few busy lanes per wave), and a lone
+ * lane running both channels of a stereo chunk is bound by the wave's
+ * instruction issue, not by the predictor's dependency chain.  So each
+ * channel gets its own lane (lanes 2k, 2k+1 of a wave for stereo chunk k;
+ * one instruction stream advances both), and the step uses a shorter chain:
+ *
+ *   t + trunc(g / 256) = med3(floor(ha / 256), floor(hb / 256), t)
+ *   with ha = g + 256 t, hb = ha + 255
+ *
+ * (floor <= trunc <= ceil and trunc is the one nearest zero, i.e. the median
+ * of floor, ceil and 0; adding t and scaling by 256 commute with the median).
+ * The int16 clamp folds in as med3(min(ha, HI), max(hb, LO), 256 t) with
+ * LO = -32768 * 256 and HI = 32767 * 256 + 255, because 256 t already lies
+ * in [LO, HI].  p1*K1 + 256 t is ready a step early, so the chain is
+ * mad24, max, med3, ashr: four operations instead of seven.
+ */
+__device__ __forceinline__ int32_t
+xa_med3(int32_t a, int32_t b, int32_t c)
+{
+	int32_t d;
+	asm("v_med3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+	return d;
+}
+
+__device__ __forceinline__ int32_t
+xa_step_lat(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
+    int32_t &p1)
+{
+	const int32_t t256 = (top >> sh) << 8;
+	const int32_t c = __mul24(p1, k1) + t256;
+	const int32_t ha = __mul24(p0, k0) + c;
+	const int32_t hb = __mul24(p0, k0) + (c + 255);
+	const int32_t s = xa_med3(min(ha, 32767 * 256 + 255),
+	    max(hb, -32768 * 256), t256) >> 8;
+	p1 = p0;
+	p0 = s;
+	return s;
+}
+
+/* value of the other lane of this lane's pair (lanes 2k <-> 2k+1) */
+__device__ __forceinline__ uint32_t
+pair_swap(uint32_t v)
+{
+	/* DPP quad_perm [1, 0, 3, 2] */
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);
+}
+
+/*
+ * Re-decode channel c of chunk q from that channel's state `sc`, rewriting
+ * its PCM; run by CH lanes together (the pair for stereo), which take the
+ * same path.  Stops once a block-end state equals the stored trajectory's
+ * in every channel (nothing after it can change).  Returns true if it met
+ * the stored trajectory; otherwise returns the chunk's new exit state in
+ * `exit` (both channels, every lane) and lane c == 0 stores it in e[q].
+ *
+ * No load sits under a branch (hipcc drains vmcnt(0) right after such
+ * loads): the next block's window and old end state are fetched every
+ * iteration with clamped addresses, one block ahead.
  */
 template <int BITS, int CH>
 __device__ bool
-fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
+fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 {
 	typedef geo<BITS, CH> g;
-	constexpr int G = g::G, OB = g::OB, WD = g::WD;
-	int32_t p0[CH], p1[CH];
-	xa_unpack_state(s.x, p0[0], p1[0]);
-	if (CH == 2)
-		xa_unpack_state(s.y, p0[CH - 1], p1[CH - 1]);
+	constexpr int BSZ = g::BSZ, EBSZ = g::EBSZ, OB = g::OB;
+	constexpr int WN = (BSZ + 3) / 4;	/* dwords of one channel block */
+	int32_t p0, p1;
+	xa_unpack_state(sc, p0, p1);
 	const int64_t eblocks = a.eblocks;
 	const int64_t b0 = (int64_t)q * a.C;
 	int64_t b1 = b0 + a.C;
 	if (b1 > eblocks)
 		b1 = eblocks;
-	auto none = [](int) {};
+	const int64_t ndw = (eblocks * EBSZ + 3) / 4;
+	const uint32_t *src = (const uint32_t *)a.src;
 
-	/*
-	 * Latency is what matters here (one busy lane per wave), so no load
-	 * sits under a divergent branch -- hipcc drains vmcnt(0) right after
-	 * such loads.  Every load is issued unconditionally with clamped
-	 * indices (results past the chunk are never used), one group ahead:
-	 * the next eblock's window and the next group's old block-end states.
-	 * The decode lands in registers; only the stores are predicated.
-	 */
-	const int64_t ndw = (eblocks * g::EBSZ + 3) / 4;	/* source dwords */
-	uint32_t buf[2][WD];
-	/* old trajectory's block-end states (frames 30, 31) of a group, read
-	 * before any rewrite; only used where b + 1 < eblocks */
-	uint32_t old[G][CH], nxt[G][CH];
-	auto rd = [&](uint32_t (*o_)[CH], int64_t bg) {
-		auto one = [&](auto uc) {
-			constexpr int u = decltype(uc)::value;
-			const int64_t b = min(bg + u, eblocks - 1);
-			const uint8_t *o = a.dst + b * OB;
-			if (CH == 2) {
-				uint2 f = *(const uint2 *)(o + 30 * 4);
-				o_[u][0] = (f.y & 0xffffu) | (f.x << 16);
-				o_[u][CH - 1] = (f.y >> 16) | (f.x & 0xffff0000u);
-			} else {
-				uint32_t f = *(const uint32_t *)(o + 30 * 2);
-				o_[u][0] = (f >> 16) | (f << 16);
-			}
-		};
-		sfor<0, G>::run(one);
+	uint32_t raw[WN + 1], nraw[WN + 1];
+	auto fetch = [&](uint32_t *r, int64_t b) {
+		const int64_t d0 = (b * EBSZ + c * BSZ) >> 2;
+#pragma unroll
+		for (int i = 0; i <= WN; i++)
+			r[i] = src[min(d0 + i, ndw - 1)];
 	};
+	/* old end state (frames 30, 31) of channel c of block b */
+	auto old_state = [&](int64_t b) -> uint32_t {
+		const uint8_t *o = a.dst + min(b, eblocks - 1) * OB;
+		if (CH == 2) {
+			const uint2 f = *(const uint2 *)(o + 30 * 4);
+			const uint32_t s1 = c ? f.x >> 16 : f.x & 0xffffu;
+			const uint32_t s0 = c ? f.y >> 16 : f.y & 0xffffu;
+			return s0 | (s1 << 16);
+		}
+		const uint32_t f = *(const uint32_t *)(o + 30 * 2);
+		return (f >> 16) | (f << 16);
+	};
+	/* decode channel c of the block whose window is r; returns this
+	 * lane's 64-B share of the block's PCM in F: stereo frames
+	 * 16c..16c+15 (the other channel's samples come from the pair lane),
+	 * or the whole mono block */
+	auto decode = [&](const uint32_t *r, int64_t b, uint32_t *F) {
+		const uint32_t o = (uint32_t)(b * EBSZ + c * BSZ) & 3u;
+		uint32_t w[WN];
+#pragma unroll
+		for (int i = 0; i < WN; i++)
+			w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], o);
+		const uint32_t prof = w[0] & 0xffu;
+		const uint32_t sh = 16u + (prof & 15u);
+		int32_t k0, k1;
+		xa_gain((prof >> 4) & 7u, k0, k1);
+		/* P[j]: samples 2j, 2j+1 of this channel */
+		uint32_t P[16];
+#pragma unroll
+		for (int j = 0; j < 16; j++) {
+			const int32_t sa = xa_step_lat(code_at<BITS>(w, 0, 2 * j), sh,
+			    k0, k1, p0, p1);
+			const int32_t sb = xa_step_lat(code_at<BITS>(w, 0, 2 * j + 1),
+			    sh, k0, k1, p0, p1);
+			P[j] = __builtin_amdgcn_perm((uint32_t)sb, (uint32_t)sa,
+			    0x05040100u);
+		}
+		if (CH == 2) {
+#pragma unroll
+			for (int j = 0; j < 8; j++) {
+				const uint32_t x = c ? P[j] : P[j + 8];
+				const uint32_t y = c ? P[j + 8] : P[j];
+				const uint32_t rv = pair_swap(x);
+				const uint32_t lp = c ? rv : y, rp = c ? y : rv;
+				F[2 * j] = __builtin_amdgcn_perm(rp, lp, 0x05040100u);
+				F[2 * j + 1] = __builtin_amdgcn_perm(rp, lp,
+				    0x07060302u);
+			}
+		} else {
+#pragma unroll
+			for (int j = 0; j < 16; j++)
+				F[j] = P[j];
+		}
+	};
+	/* whole blocks in the loop (always four 16-B stores, so the wait
+	 * for the prefetched window can leave them in flight); the stream's
+	 * cut last block, if it is this chunk's, after it */
+	const int64_t nfull = (int64_t)(a.pcm_bytes / OB);
+	const int64_t bf = min(b1, nfull);
+	fetch(raw, b0);
+	uint32_t old = old_state(b0);
 	bool met = false;
-	load_window<BITS, CH, 0>(buf[0], a.src, b0);
-	rd(old, b0);
-	for (int64_t bg = b0; bg < b1; bg += G) {
-		rd(nxt, bg + G);
-		auto body = [&](auto uc) {
-			constexpr int u = decltype(uc)::value;
-			const int64_t b = bg + u;
-			/* prefetch eblock b + 1's window (clamped: past the
-			 * stream's end it is never used) */
-			load_window_clamped<BITS, CH, (u + 1) % G>(buf[(u + 1) & 1],
-			    a.src, b + 1, ndw);
-			const bool act = !met && b < b1;
-			int32_t q0[CH], q1[CH];
+	int64_t b = b0;
+	for (; b < bf; b++) {
+		fetch(nraw, b + 1);
+		const uint32_t nold = old_state(b + 1);
+		uint32_t F[16];
+		decode(raw, b, F);
+		u32x4a *d = (u32x4a *)(a.dst + (uint64_t)b * OB + (uint64_t)c * 64u);
 #pragma unroll
-			for (int c = 0; c < CH; c++) {
-				q0[c] = p0[c];
-				q1[c] = p1[c];
+		for (int i = 0; i < 4; i++) {
+			u32x4a v = { F[4 * i], F[4 * i + 1], F[4 * i + 2],
+			    F[4 * i + 3] };
+			d[i] = v;
+		}
+		if (b + 1 < eblocks) {
+			uint32_t m = xa_pack_state(p0, p1) == old;
+			if (CH == 2)
+				m &= pair_swap(m);
+			if (m) {
+				met = true;
+				break;
 			}
-			uint32_t out[OB / 4] __attribute__((aligned(16)));
-			(void)decode_eblock<BITS, CH, true, false, 64>(buf[u & 1],
-			    g::woff(u), p0, p1, (uint8_t *)out, none);
-			if (act) {
-				uint8_t *d = a.dst + b * OB;
-				if ((uint64_t)(b + 1) * OB <= a.pcm_bytes) {
+		}
 #pragma unroll
-					for (int i = 0; i < OB / 16; i++)
-						((u32x4a *)d)[i] = ((const u32x4a *)out)[i];
-				} else {
-					/* the stream's cut last eblock */
-#pragma unroll
-					for (int k = 0; k < OB / 4; k++) {
-						const uint64_t off = (uint64_t)b * OB + 4u * k;
-						if (off + 4u <= a.pcm_bytes)
-							*(uint32_t *)(a.dst + off) = out[k];
-						else if (off < a.pcm_bytes)
-							*(uint16_t *)(a.dst + off) =
-							    (uint16_t)out[k];
-					}
-				}
-			}
-#pragma unroll
-			for (int c = 0; c < CH; c++) {
-				p0[c] = act ? p0[c] : q0[c];
-				p1[c] = act ? p1[c] : q1[c];
-			}
-			if (act && b + 1 < eblocks) {
-				bool m = true;
-#pragma unroll
-				for (int c = 0; c < CH; c++)
-					m = m && xa_pack_state(p0[c], p1[c]) == old[u][c];
-				met = m;
-			}
-		};
-		sfor<0, G>::run(body);
-		if (met)
-			break;
-#pragma unroll
-		for (int u = 0; u < G; u++)
-#pragma unroll
-			for (int c = 0; c < CH; c++)
-				old[u][c] = nxt[u][c];
+		for (int i = 0; i <= WN; i++)
+			raw[i] = nraw[i];
+		old = nold;
+	}
+	if (!met && b < b1) {
+		/* b == eblocks - 1, PCM cut short: no later block to meet */
+		uint32_t F[16];
+		decode(raw, b, F);
+		const uint64_t off = (uint64_t)b * OB + (uint64_t)c * 64u;
+		uint8_t *d = a.dst + off;
+		for (int k = 0; k < 16; k++) {
+			if (off + 4u * k + 4u <= a.pcm_bytes)
+				((uint32_t *)d)[k] = F[k];
+			else if (off + 4u * k < a.pcm_bytes)
+				((uint16_t *)d)[2 * k] = (uint16_t)F[k];
+		}
 	}
 	if (met)
 		return true;
-	exit.x = xa_pack_state(p0[0], p1[0]);
-	exit.y = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
-	a.e[q] = exit;
+	const uint32_t st = xa_pack_state(p0, p1);
+	if (CH == 2) {
+		const uint32_t other = pair_swap(st);
+		exit.x = c ? other : st;
+		exit.y = c ? st : other;
+	} else {
+		exit.x = st;
+		exit.y = 0u;
+	}
+	if (c == 0)
+		a.e[q] = exit;
 	return false;
 }
 
@@ -626,30 +695,43 @@ heap_pop(uint32_t *h, uint32_t &n)
 }
 
 /*
- * The sequential tail (one thread): drain the re-check queue in chunk order
- * (a heap, so even a pathological cascade costs O(n log n) bookkeeping),
- * then publish the status words and reset the control words.
+ * The sequential tail (the first CH lanes of one wave: repairs run a lane
+ * per channel; the heap lives in lane 0): drain the re-check queue in chunk
+ * order (a heap, so even a pathological cascade costs O(n log n)
+ * bookkeeping), then publish the status words and reset the control words.
+ * Queue entries are >= 1, so 0 ends the loop.
  */
 template <int BITS, int CH>
 __device__ void
 drain_tail(const xa_dec_args &a)
 {
+	const int c = threadIdx.x;
 	const uint32_t nq = a.ctl[XA_CTL_NQ];
 	uint32_t n = 0, tail = 0;
-	for (uint32_t i = 0; i < nq; i++)
-		heap_push(a.queue, n, a.queue[i]);
-	while (n > 0) {
-		const uint32_t q = heap_pop(a.queue, n);
+	if (c == 0)
+		for (uint32_t i = 0; i < nq; i++)
+			heap_push(a.queue, n, a.queue[i]);
+	for (;;) {
+		uint32_t q = 0;
+		if (c == 0 && n > 0)
+			q = heap_pop(a.queue, n);
+		q = __builtin_amdgcn_readfirstlane(q);
+		if (q == 0)
+			break;
 		const uint2 s = a.e[q - 1], gq = a.g[q];
 		if (s.x == gq.x && s.y == gq.y)
 			continue;
 		tail++;
 		uint2 ex;
-		const bool met = fix_chunk<BITS, CH>(a, q, s, ex);
-		a.g[q] = s;
-		if (!met && q + 1 < a.nchunks)
-			heap_push(a.queue, n, q + 1);
+		const bool met = fix_lane<BITS, CH>(a, q, c, c ? s.y : s.x, ex);
+		if (c == 0) {
+			a.g[q] = s;
+			if (!met && q + 1 < a.nchunks)
+				heap_push(a.queue, n, q + 1);
+		}
 	}
+	if (c != 0)
+		return;
 	const uint2 fin = a.e[a.nchunks - 1];
 	a.status[XA_ST_ERR] = a.ctl[XA_CTL_ERR];
 	a.status[XA_ST_STATE_L] = fin.x;
@@ -719,13 +801,18 @@ xa_decode_fix(xa_dec_args a)
 		}
 		__syncthreads();
 		const uint32_t nf = nfix;
-		for (uint32_t k = threadIdx.x; k < nf; k += 256u) {
+		/* a lane per channel: stereo chunk k on lanes 2k, 2k+1 */
+		const int c = threadIdx.x % CH;
+		for (uint32_t k = threadIdx.x / CH; k < nf; k += 256u / CH) {
 			const uint32_t q = fixq[k];
 			const uint2 s = fixs[k];
 			uint2 ex;
-			const bool met = fix_chunk<BITS, CH>(a, q, s, ex);
-			a.g[q] = s;
+			const bool met = fix_lane<BITS, CH>(a, q, c, c ? s.y : s.x,
+			    ex);
 			wrote = true;
+			if (c != 0)
+				continue;
+			a.g[q] = s;
 			if (!met && q + 1 < n) {
 				uint32_t i = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
 				a.queue[i] = q + 1;
@@ -749,7 +836,7 @@ xa_decode_fix(xa_dec_args a)
 		last = atomicAdd(&a.ctl[XA_CTL_TICKET], 1u) == gridDim.x - 1;
 	}
 	__syncthreads();
-	if (!last || threadIdx.x != 0)
+	if (!last || threadIdx.x >= CH)
 		return;
 	/* acquire: this CU now sees every other workgroup's writes */
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -792,8 +879,10 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 	}
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
+#if !defined(XA_DBG_STEP) && !defined(XA_DBG_NOSTORE)
 	hipLaunchKernelGGL((xa_decode_fix<BITS, CH>), dim3(grid2), dim3(256), 0,
 	    st, a);
+#endif
 	return hipGetLastError();
 }
 
