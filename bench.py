@@ -53,6 +53,24 @@ def hip_runtime():
     return L
 
 
+def reduce_over_ranks(elapsed, ok, dev):
+    """Whole-job view of one rank's result: the max of the timed region over
+    ranks and the AND of the bit-exact checks (None = not checked counts as
+    passing).  RCCL on the GPU box; the gloo test runs it on CPU tensors."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    okt = torch.tensor([1 if ok in (None, True) else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    return float(t.item()), (bool(okt.item()) if ok is not None else None)
+
+
+def job_value(samples_per_rank, world, steps, elapsed):
+    """MSamples/s of the whole job: every rank decodes its own stream."""
+    return samples_per_rank * world * steps / elapsed / 1e6
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,10 +137,6 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     spec_ms = []
     for a, b in evs[args.warmup:]:
@@ -157,15 +171,14 @@ def main():
                    "sample": "the full %s stream (%d samples), oracle/xa_oracle.c "
                              "single-pass decode, 1 thread, best of 3" % (args.workload, samples)}
     if world > 1:
-        okt = torch.tensor([1 if ok in (None, True) else 0], device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item()) if ok is not None else None
+        elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
 
     xa_bytes = eb * ch * (bits * 4 + 1)
     pcm_bytes = eb * 64 * ch
     alg_bytes = xa_bytes + pcm_bytes
     achieved = alg_bytes / (spec_avg_ms * 1e-3) / 1e9
     traffic = None
+    traffic_src = None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
         try:
@@ -173,11 +186,11 @@ def main():
                 p = json.load(f)
             if p.get("workload") == args.workload and p.get("mix") == args.mix:
                 traffic = p.get("hbm_bytes_per_launch")
+                traffic_src = p.get("source")
         except (OSError, ValueError):
             traffic = None
 
-    total_samples = samples * world * args.steps
-    value = total_samples / elapsed / 1e6
+    value = job_value(samples, world, args.steps, elapsed)
     line = {
         "metric": "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs CPU",
         "value": round(value, 1),
@@ -191,15 +204,16 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (seeded XA stream, profile mix %s, uniform codes)" % args.mix,
-        "config": {"workload": desc + " per rank", "bits": bits, "channels": ch,
+        "config": {"workload": desc + " per rank", "workload_id": args.workload,
+                   "bits": bits, "channels": ch,
                    "eblocks_per_rank": eb, "samples_per_rank": samples,
                    "profile_mix": args.mix, "parallelism": "independent streams, 1 per GPU",
-                   "chunk": args.chunk or "auto", "warmup_eblocks": args.warm_blocks
-                   if args.warm_blocks >= 0 else "auto"},
+                   "chunk": int(st[6]), "warmup_eblocks": int(st[7]),
+                   "tuning": "auto" if not args.chunk and args.warm_blocks < 0 else "manual"},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_per_launch": alg_bytes, "traffic_source": traffic_src,
                      "launch_ms": round(spec_avg_ms, 4)},
         "cpu_baseline": cpu,
         "bit_exact": ok,

@@ -21,6 +21,8 @@
 #define XA_ST_FIXED	3
 #define XA_ST_TAIL	4
 #define XA_ST_CHUNKS	5
+#define XA_ST_C		6
+#define XA_ST_W		7
 #define XA_ST_WORDS	8
 
 struct xa_dec_args {

@@ -739,6 +739,8 @@ drain_tail(const xa_dec_args &a)
 	a.status[XA_ST_FIXED] = a.ctl[XA_CTL_FIXED];
 	a.status[XA_ST_TAIL] = tail;
 	a.status[XA_ST_CHUNKS] = a.nchunks;
+	a.status[XA_ST_C] = a.C;
+	a.status[XA_ST_W] = a.W;
 	a.ctl[XA_CTL_ERR] = 0xffffffffu;
 	a.ctl[XA_CTL_NQ] = 0;
 	a.ctl[XA_CTL_FIXED] = 0;

@@ -5,10 +5,9 @@
  * The reference has one hot-path entry per direction, bjxa_decode()
  * (src/libbjxa.c:602-661) and bjxa_encode() (:759-819), both on host
  * buffers, one stream at a time.  These entries take device pointers so a
- * caller that keeps streams in HBM pays no PCIe copy, accept many streams
- * per launch, and accept an explicit entry state -- the same thing the
- * reference expresses through the befL/befR header fields (:417-420) to
- * resume or segment a stream.
+ * caller that keeps streams in HBM pays no PCIe copy, and accept an
+ * explicit entry state -- the same thing the reference expresses through
+ * the befL/befR header fields (:417-420) to resume or segment a stream.
  *
  * All pointers named d_* are device pointers on the current HIP device;
  * `stream` is a hipStream_t (NULL = default stream).  Calls are
@@ -55,7 +54,7 @@ typedef struct {
  *  [1] exit state L (prev[0] | prev[1] << 16)
  *  [2] exit state R
  *  [3] chunks repaired by the verify pass, [4] by the sequential tail,
- *  [5] chunks
+ *  [5] chunks, [6] chunk length and [7] warm-up length used (eblocks)
  */
 #define BJXA_HIP_STATUS_WORDS 8
 
@@ -65,7 +64,7 @@ size_t bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
     const bjxa_hip_tuning_t *tune);
 int bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream);
 
-/* decode one stream (three kernels on `stream`, no host sync) */
+/* decode one stream (two kernels on `stream`, no host sync) */
 int bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws,
     size_t ws_len, uint32_t *d_status, const bjxa_hip_tuning_t *tune,
     void *stream);

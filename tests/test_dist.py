@@ -1,0 +1,75 @@
+"""The multi-GPU bench path on CPU: world_size 2 over gloo.
+
+bench.py shards by stream (every rank decodes its own seeded stream, no
+data-path collective) and reduces only the timed region (max) and the
+bit-exact flags (AND) across ranks.  These tests run that reduction and the
+per-rank workload derivation in two gloo processes.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from bjxa_amd import synth
+        dev = torch.device("cpu")
+        # rank r times 1.0 + r seconds; rank 1 fails its check in round 2
+        t, ok = bench.reduce_over_ranks(1.0 + rank, True, dev)
+        t2, ok2 = bench.reduce_over_ranks(0.5, rank != 1, dev)
+        t3, ok3 = bench.reduce_over_ranks(0.25, None, dev)
+        # each rank's stream: C3-shaped, seeded by rank
+        xa = synth.stream(1000, 8, 2, "A", seed=rank)
+        h = int(np.bitwise_xor.reduce(xa.view(np.uint64)))
+        ht = torch.tensor([h & 0x7fffffffffffffff], dtype=torch.int64)
+        hs = [torch.zeros_like(ht) for _ in range(world)]
+        dist.all_gather(hs, ht)
+        q.put((rank, t, ok, t2, ok2, t3, ok3, [int(x.item()) for x in hs]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_reduction_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, t, ok, t2, ok2, t3, ok3, hs in res:
+        assert t == 2.0 and ok is True          # max over ranks
+        assert t2 == 0.5 and ok2 is False       # one failing rank fails the job
+        assert ok3 is None                       # unchecked stays unchecked
+        assert hs[0] != hs[1]                   # ranks decode different streams
+
+
+def test_job_value_weak_scaling():
+    import bench
+    # 2 ranks x 320M samples x 20 steps in 10 ms
+    assert bench.job_value(320_000_000, 2, 20, 0.01) == pytest.approx(1.28e6)
+    # per-GPU work fixed: doubling ranks at equal time doubles the value
+    assert bench.job_value(1, 4, 1, 1.0) == 2 * bench.job_value(1, 2, 1, 1.0)

@@ -1,11 +1,20 @@
-"""Summarise tools/profile.sh output: per-kernel mean duration (kernel trace)
-and per-dispatch mean of every PMC counter for the decode kernels.
+"""Summarise tools/profile.sh output.
 
 usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [--json out.json]
-HBM bytes: FETCH_SIZE and WRITE_SIZE are in KiB (x1024).  MI355X_MICROARCH.md
-§HBM: on gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide coalesced
-streaming read; the raw value is reported and the x2 correction is applied
-only where stated.
+
+  kernel_us      per-kernel mean duration from the kernel trace of the bench
+                 command (trace/), and kernel_n the dispatch counts
+  pmc            per-kernel, per-dispatch mean of every counter (pmc*/)
+  traffic        HBM bytes per xa_decode_spec launch:
+                   write = WRITE_SIZE x 1 KiB (MI355X_MICROARCH.md §HBM: exact
+                           for 16-B/lane streaming stores, which these are)
+                   read  = TCC_EA0_RDREQ x bytes-per-request, the latter
+                           calibrated on this kernel's own load pattern by the
+                           warm-up-0 pass (pmc_w0/), which loads exactly the
+                           XA stream once: bytes_per_rdreq = XA bytes /
+                           RDREQ(w0).  FETCH_SIZE raw (x1 KiB) and the
+                           guide's x2 rule for 16-B/lane reads are reported
+                           beside it for comparison.
 """
 import csv
 import glob
@@ -16,39 +25,64 @@ from collections import defaultdict
 
 
 def rows(pattern):
-    for f in glob.glob(pattern, recursive=True):
+    for f in sorted(glob.glob(pattern, recursive=True)):
         with open(f) as fh:
             yield from csv.DictReader(fh)
 
 
 def short(name):
-    for k in ("xa_decode_spec", "xa_decode_fix", "xa_decode_tail", "xa_encode_groups"):
+    for k in ("xa_decode_spec", "xa_decode_fix", "xa_encode_groups", "xa_ws_init"):
         if k in name:
             return k
     return name[:40]
 
 
+def counters(pattern):
+    pmc = defaultdict(lambda: defaultdict(list))
+    for r in rows(pattern):
+        pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in pmc.items()}
+
+
 def main():
     d = sys.argv[1]
     out = {}
+    bench = None
+    bj = os.path.join(d, "bench.json")
+    if os.path.exists(bj):
+        lines = [ln for ln in open(bj).read().splitlines() if ln.startswith("{")]
+        if lines:
+            bench = json.loads(lines[-1])
+            out["bench"] = bench
     dur = defaultdict(list)
     for r in rows(os.path.join(d, "trace", "**", "*kernel_trace.csv")):
         dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     out["kernel_us"] = {k: round(sum(v) / len(v) / 1e3, 2) for k, v in dur.items()}
     out["kernel_n"] = {k: len(v) for k, v in dur.items()}
-    pmc = defaultdict(lambda: defaultdict(list))
-    for r in rows(os.path.join(d, "pmc*", "**", "*counter_collection.csv")):
-        pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    out["pmc"] = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in pmc.items()}
+    out["pmc"] = counters(os.path.join(d, "pmc[0-9]*", "**", "*counter_collection.csv"))
+    w0 = counters(os.path.join(d, "pmc_w0", "**", "*counter_collection.csv"))
+    out["pmc_w0"] = w0
     sp = out["pmc"].get("xa_decode_spec", {})
-    if "FETCH_SIZE" in sp and "WRITE_SIZE" in sp:
-        out["spec_fetch_bytes_raw"] = sp["FETCH_SIZE"] * 1024
-        out["spec_write_bytes"] = sp["WRITE_SIZE"] * 1024
+    if bench and "TCC_EA0_RDREQ_sum" in sp and "TCC_EA0_RDREQ_sum" in w0.get("xa_decode_spec", {}):
+        cfg = bench["config"]
+        xa_bytes = cfg["eblocks_per_rank"] * cfg["channels"] * (cfg["bits"] * 4 + 1)
+        bpr = xa_bytes / w0["xa_decode_spec"]["TCC_EA0_RDREQ_sum"]
+        read = sp["TCC_EA0_RDREQ_sum"] * bpr
+        write = sp.get("WRITE_SIZE", 0.0) * 1024
+        t = {"read_bytes": round(read), "write_bytes": round(write),
+             "hbm_bytes_per_launch": round(read + write),
+             "bytes_per_rdreq": round(bpr, 2),
+             "alg_bytes_per_launch": xa_bytes + cfg["eblocks_per_rank"] * 64 * cfg["channels"]}
+        if "FETCH_SIZE" in sp:
+            t["fetch_size_raw_bytes"] = round(sp["FETCH_SIZE"] * 1024)
+            t["fetch_size_x2_bytes"] = round(sp["FETCH_SIZE"] * 2048)
+        t["traffic_over_alg"] = round(t["hbm_bytes_per_launch"] / t["alg_bytes_per_launch"], 4)
+        out["traffic"] = t
     js = json.dumps(out, indent=1, sort_keys=True)
     print(js)
     if "--json" in sys.argv:
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
-            f.write(js)
+            f.write(js + "\n")
 
 
 if __name__ == "__main__":
