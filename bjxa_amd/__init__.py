@@ -272,8 +272,14 @@ def encode_wav(data, bits=6):
 
 # ---- device-resident extension (include/bjxa_hip.h) ----------------------
 
-def decode_workspace_size(eblocks, channels, chunk=0, warmup=-1):
+VARIANT_BALANCED = 0x20   # two-length chunk plan (include/bjxa_hip.h)
+
+
+def decode_workspace_size(eblocks, channels, chunk=0, warmup=-1, variant=0):
+    """bjxa_hip_decode_workspace: device workspace bytes for one stream
+    (pass the same chunk/warmup/variant as the decode)."""
     t = HipTuning(chunk, warmup)
+    t.variant = variant
     return lib().bjxa_hip_decode_workspace(eblocks, channels, ctypes.byref(t))
 
 

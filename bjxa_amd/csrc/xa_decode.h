@@ -32,6 +32,9 @@ struct xa_dec_args {
 	uint32_t eblocks;
 	uint32_t nchunks;
 	uint32_t C, W;		/* chunk and warm-up lengths in eblocks */
+	uint32_t nlong;		/* chunks [0, nlong) are C + G long (G = 4 / ch,
+				 * nlong % 64 == 0); chunk q starts at eblock
+				 * q*C + G*min(q, nlong) */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
 	uint2 *g, *e;		/* per-chunk entry / exit state */
 	uint32_t *queue;	/* re-check queue, nchunks entries */

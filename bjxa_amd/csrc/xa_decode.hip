@@ -106,15 +106,26 @@ template <int BITS, int CH> struct geo {
 	static constexpr int NP = SEGB / PS;		/* pieces per segment */
 };
 
+/* first eblock of chunk q (chunks [0, nlong) are G longer) */
+template <int G>
+__device__ __forceinline__ int64_t
+chunk_start(const xa_dec_args &a, uint32_t q)
+{
+	return (int64_t)q * a.C + (int64_t)G * min(q, a.nlong);
+}
+
 /*
  * Decode the channel blocks of one eblock whose first byte is byte O of w,
  * advancing the lane's state.  With STORE the output goes to `line` in
- * 16-B pieces; after every LB bytes `flush(h)` runs (h = LB-byte line
- * index), and with RESTART the next line is written at `line` again (LDS
- * staging), otherwise output continues at line + LB (direct stores).
- * Returns a bit per channel whose gain nibble is >= 5.
+ * 16-B pieces, numbered from QB (the eblock's first piece within the
+ * group); after every LB bytes `flush(h)` runs (h = LB-byte line index
+ * within the group), and with RESTART the next line is written at `line`
+ * again (LDS staging), otherwise output continues at line + LB (direct
+ * stores).  A line may span eblocks (mono: 64 B per block).  Returns a bit
+ * per channel whose gain nibble is >= 5.
  */
-template <int BITS, int CH, bool STORE, bool RESTART, int LB, typename F>
+template <int BITS, int CH, bool STORE, bool RESTART, int LB, int QB = 0,
+    typename F>
 __device__ __forceinline__ uint32_t
 decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
     uint8_t *line, F &flush)
@@ -159,9 +170,10 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		if (STORE) {
 			u32x4a v = { fr[0], fr[1], fr[2], fr[3] };
 			constexpr int QL = LB / 16;	/* pieces per line */
-			*(u32x4a *)(line + 16 * (RESTART ? (q % QL) : q)) = v;
-			if (q % QL == QL - 1)
-				flush(q / QL);
+			const int qq = QB + q;
+			*(u32x4a *)(line + 16 * (RESTART ? (qq % QL) : qq)) = v;
+			if (qq % QL == QL - 1)
+				flush(qq / QL);
 		}
 		/* keep the unpack of later codes from being hoisted here: it
 		 * would only raise register pressure */
@@ -172,7 +184,8 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 
 /*
  * Store the wave's staged LB-byte lines: line j belongs to chunk
- * wchunk0 + j and goes to byte `rel_off` of that chunk's PCM.  Lane l
+ * wchunk0 + j (whose PCM starts at wstart_b + j * chunk_bytes) and goes to
+ * byte `rel_off` of that chunk's PCM.  Lane l
  * stores piece l % P of lines l / P + (64 / P) i (P = LB / 16 pieces per
  * line).  Wave-uniform fast path when every line is whole; otherwise (the
  * grid's last wave only) per-piece bounds and a 2-byte tail for the
@@ -181,8 +194,8 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 template <int LB, bool NT>
 __device__ __forceinline__ void
 store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
-    uint32_t wchunk0, uint32_t chunk_bytes, uint32_t rel_off, bool wave_full,
-    uint8_t *gbase, const uint8_t *lbase)
+    uint32_t wchunk0, uint64_t wstart_b, uint32_t chunk_bytes, uint32_t rel_off,
+    bool wave_full, uint8_t *gbase, const uint8_t *lbase)
 {
 	constexpr int LINE = LB + 16, P = LB / 16, LPI = 64 / P;
 #ifdef XA_DBG_NOSTORE
@@ -207,15 +220,15 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 	/* launder the inputs so none of this rare path's address arithmetic
 	 * is hoisted out of the caller's loops (it would pin ~100 VGPRs) */
 	uint32_t wc = wchunk0, nch = a.nchunks, cb = chunk_bytes, ro = rel_off;
-	uint64_t lim = a.pcm_bytes;
+	uint64_t lim = a.pcm_bytes, wsb = wstart_b;
 	uint8_t *dst = a.dst;
 	asm volatile("" : "+v"(wc), "+v"(nch), "+v"(cb), "+v"(ro), "+v"(lim),
-	    "+v"(dst));
+	    "+v"(dst), "+v"(wsb));
 #pragma nounroll
 	for (int i = 0; i < P; i++) {
 		const int j = i * LPI + lane / P, pc = lane % P;
 		const uint32_t cj = wc + (uint32_t)j;
-		const uint64_t off = (uint64_t)cj * cb + ro + (uint64_t)pc * 16u;
+		const uint64_t off = wsb + (uint64_t)j * cb + ro + (uint64_t)pc * 16u;
 		if (cj >= nch)
 			continue;
 		const uint8_t *from = obuf + j * LINE + pc * 16;
@@ -253,20 +266,20 @@ dma<16>(const void *g, uint8_t *l)
  * the 64 segments (SEGB bytes each) are concatenated and cut into PS-byte
  * pieces; instruction i moves pieces [64i, 64i+64) of that concatenation
  * (lane t: piece 64i+t), i.e. 64*PS contiguous bytes of one or two
- * segments.
+ * segments.  The wave's chunks start at eblock wstart and are Cw long.
  * `rel` is the group's first eblock relative to each chunk's start.
  * Segments outside the stream (warm-up before eblock 0, the ragged end) are
  * clamped onto valid bytes; their lanes never decode them.
  */
 template <int BITS, int CH>
 __device__ __forceinline__ void
-stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, uint32_t wchunk0,
-    int64_t rel, const uint32_t *voff)
+stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, int64_t wstart,
+    uint32_t Cw, int64_t rel, const uint32_t *voff)
 {
 	typedef geo<BITS, CH> g;
 	constexpr int NP = g::NP, PS = g::PS;
-	const int64_t e_first = (int64_t)wchunk0 * a.C + rel;
-	const int64_t e_end = (int64_t)(wchunk0 + 63u) * a.C + rel + g::G;
+	const int64_t e_first = wstart + rel;
+	const int64_t e_end = wstart + 63 * (int64_t)Cw + rel + g::G;
 	/* the last segment's read may run SEGB - 4*GDW bytes past its group */
 	if (e_first >= 0 && e_end * g::EBSZ + (g::SEGB - 4 * g::GDW) <=
 	    (int64_t)a.eblocks * g::EBSZ) {
@@ -281,16 +294,16 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, uint32_t wchunk0,
 	 * dword holding the stream's last byte is read whole, nothing past
 	 * it).  Launder the inputs so none of its arithmetic is hoisted into
 	 * the caller's loops. */
-	uint32_t wc = wchunk0, C = a.C, neb = a.eblocks;
-	int64_t r = rel;
+	uint32_t C = Cw, neb = a.eblocks;
+	int64_t r = wstart + rel;
 	const uint8_t *src = a.src;
-	asm volatile("" : "+v"(wc), "+v"(C), "+v"(neb), "+v"(r), "+v"(src));
+	asm volatile("" : "+v"(C), "+v"(neb), "+v"(r), "+v"(src));
 	constexpr int SD = g::SEGB / 4;
 	const int64_t last = ((int64_t)neb * g::EBSZ - 1) & ~(int64_t)3;
 #pragma nounroll
 	for (int i = 0; i < SD; i++) {
 		const int k = i * 64 + lane, seg = k / SD, off = k % SD;
-		int64_t byte = ((int64_t)(wc + seg) * C + r) * g::EBSZ + off * 4;
+		int64_t byte = ((int64_t)seg * C + r) * g::EBSZ + off * 4;
 		byte = byte < 0 ? 0 : (byte > last ? last : byte);
 		dma<4>(src + byte, ibuf + i * 256);
 	}
@@ -330,7 +343,10 @@ xa_decode_spec(xa_dec_args a)
 	const uint32_t wchunk0 = blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u;
 	const uint32_t chunk = wchunk0 + lane;
 	const int64_t eblocks = a.eblocks;
-	const int64_t b0 = (int64_t)chunk * a.C;
+	/* the wave's chunks are all long or all short (nlong % 64 == 0) */
+	const uint32_t Cw = a.C + (wchunk0 < a.nlong ? (uint32_t)G : 0u);
+	const int64_t wstart = chunk_start<G>(a, wchunk0);
+	const int64_t b0 = wstart + (int64_t)lane * Cw;
 	const int W = (int)a.W;
 
 	/* DMA source offsets (bytes from the wave's segment 0) of this lane's
@@ -340,7 +356,7 @@ xa_decode_spec(xa_dec_args a)
 #pragma unroll
 	for (int i = 0; i < NP; i++) {
 		const int k = i * 64 + lane;
-		voff[i] = (uint32_t)(k / NP) * a.C * EBSZ + (uint32_t)(k % NP) * PS;
+		voff[i] = (uint32_t)(k / NP) * Cw * EBSZ + (uint32_t)(k % NP) * PS;
 	}
 
 	int32_t p0[CH], p1[CH];
@@ -355,7 +371,7 @@ xa_decode_spec(xa_dec_args a)
 	uint32_t w[GDW];
 	const uint32_t *mine = (const uint32_t *)(ibuf + lane * g::SEGB);
 	auto none = [](int) {};
-	stage_group<BITS, CH>(a, ibuf, lane, wchunk0, -W, voff);
+	stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, -W, voff);
 
 	/* warm-up: state only; the next group's DMA overlaps the decode */
 	for (int rel = -W; rel < 0; rel += G) {
@@ -364,7 +380,7 @@ xa_decode_spec(xa_dec_args a)
 		for (int i = 0; i < GDW; i++)
 			w[i] = mine[i];
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-		stage_group<BITS, CH>(a, ibuf, lane, wchunk0, rel + G, voff);
+		stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, rel + G, voff);
 		auto body = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
 			const int64_t b = b0 + rel + u;
@@ -379,17 +395,18 @@ xa_decode_spec(xa_dec_args a)
 	gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
 
 	/* the chunk: decode, stage 64-B lines, write them back whole */
-	const uint32_t chunk_bytes = a.C * OB;
+	const uint32_t chunk_bytes = Cw * OB;
+	const uint64_t wstart_b = (uint64_t)wstart * OB;
 	constexpr int P = LB / 16;
-	uint8_t *gbase = a.dst + (uint64_t)(wchunk0 + lane / P) * chunk_bytes +
+	uint8_t *gbase = a.dst + wstart_b + (uint64_t)(lane / P) * chunk_bytes +
 	    (lane % P) * 16;
 	const uint8_t *lbase = obuf + (lane / P) * LINE + (lane % P) * 16;
 	/* every line of this wave lies before the stream's first cut block */
 	const uint64_t full_blocks = a.pcm_bytes / OB;
 	const bool wave_full = wchunk0 + 63u < a.nchunks &&
-	    (uint64_t)(wchunk0 + 64u) * a.C <= full_blocks;
+	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
 	bool first = true;
-	for (int s0 = 0; s0 < (int)a.C; s0 += G) {
+	for (int s0 = 0; s0 < (int)Cw; s0 += G) {
 		/* this group's DMA, not the previous group's stores */
 		if (!SPLIT || first || !wave_full)
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -401,17 +418,17 @@ xa_decode_spec(xa_dec_args a)
 		for (int i = 0; i < GDW; i++)
 			w[i] = mine[i];
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-		if (SPLIT && s0 + G < (int)a.C)
-			stage_group<BITS, CH>(a, ibuf, lane, wchunk0, s0 + G, voff);
+		if (SPLIT && s0 + G < (int)Cw)
+			stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, s0 + G, voff);
 		auto body = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
 			const int s = s0 + u;
 			const int64_t b = b0 + s;
 			auto flush = [&](int h) {
 				wave_lds_sync();
-				store_lines<LB, NT>(a, obuf, lane, wchunk0, chunk_bytes,
-				    (uint32_t)s * OB + (uint32_t)LB * h, wave_full, gbase,
-				    lbase);
+				store_lines<LB, NT>(a, obuf, lane, wchunk0, wstart_b,
+				    chunk_bytes, (uint32_t)s0 * OB + (uint32_t)LB * h,
+				    wave_full, gbase, lbase);
 				wave_lds_sync();
 			};
 			/* every lane runs the decode (flush holds wave-wide
@@ -424,8 +441,8 @@ xa_decode_spec(xa_dec_args a)
 				q0[c] = p0[c];
 				q1[c] = p1[c];
 			}
-			uint32_t bad = decode_eblock<BITS, CH, true, true, LB>(w,
-			    u * EBSZ, p0, p1, line, flush);
+			uint32_t bad = decode_eblock<BITS, CH, true, true, LB,
+			    u * 4 * CH>(w, u * EBSZ, p0, p1, line, flush);
 			if (act && bad) {
 				uint32_t cb = (uint32_t)b * CH + ((bad & 1u) ? 0u : 1u);
 				atomicMin(&a.ctl[XA_CTL_ERR], cb);
@@ -437,9 +454,9 @@ xa_decode_spec(xa_dec_args a)
 			}
 		};
 		sfor<0, G>::run(body);
-		if (!SPLIT && s0 + G < (int)a.C) {
+		if (!SPLIT && s0 + G < (int)Cw) {
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-			stage_group<BITS, CH>(a, ibuf, lane, wchunk0, s0 + G, voff);
+			stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, s0 + G, voff);
 		}
 	}
 	if (chunk < a.nchunks) {
@@ -526,8 +543,8 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 	int32_t p0, p1;
 	xa_unpack_state(sc, p0, p1);
 	const int64_t eblocks = a.eblocks;
-	const int64_t b0 = (int64_t)q * a.C;
-	int64_t b1 = b0 + a.C;
+	const int64_t b0 = chunk_start<g::G>(a, q);
+	int64_t b1 = chunk_start<g::G>(a, q + 1);
 	if (b1 > eblocks)
 		b1 = eblocks;
 	const int64_t ndw = (eblocks * EBSZ + 3) / 4;
@@ -860,25 +877,24 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 		grid2 = 256u;
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
-	/* variant bit 0: SPLIT regions; bit 1: non-temporal output stores */
-	switch (variant & 3u) {
-	case 0:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, 64 * CH, false>),
-		    dim3(grid), dim3(per), 0, st, a);
-		break;
+	/* variant bit 1: non-temporal PCM stores; bits 2-3: bytes per lane
+	 * per store phase (0: one eblock, 1: 128, 2: 256).  (SPLIT staging
+	 * regions measured no gain and are not instantiated.) */
+#define SPEC(LB, NT) hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, LB, NT>), \
+    dim3(grid), dim3(per), 0, st, a)
+	const bool nt = (variant & 2u) != 0;
+	switch ((variant >> 2) & 3u) {
 	case 1:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, true, 64 * CH, false>),
-		    dim3(grid), dim3(per), 0, st, a);
+		if (nt) SPEC(128, true); else SPEC(128, false);
 		break;
 	case 2:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, 64 * CH, true>),
-		    dim3(grid), dim3(per), 0, st, a);
+		if (nt) SPEC(256, true); else SPEC(256, false);
 		break;
 	default:
-		hipLaunchKernelGGL((xa_decode_spec<BITS, CH, true, 64 * CH, true>),
-		    dim3(grid), dim3(per), 0, st, a);
+		if (nt) SPEC(64 * CH, true); else SPEC(64 * CH, false);
 		break;
 	}
+#undef SPEC
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
 #if !defined(XA_DBG_STEP) && !defined(XA_DBG_NOSTORE)

@@ -15,15 +15,19 @@
 #include "xa_gpu.h"
 #include "../../include/bjxa_hip.h"
 
-#define DEFAULT_WARMUP	8u	/* eblocks; SURVEY App. C / DESIGN.md */
+#define DEFAULT_WARMUP	8u	/* eblocks; DESIGN.md §3 */
+#define MIN_CHUNK	16u
 /*
- * Automatic chunk length: aim for about 2 (stereo) or 4 (mono) resident
- * 256-lane workgroups per CU on the 256 CUs -- the speculative kernel is
- * throughput-bound per CU, so its time goes as (workgroups on the busiest
- * CU) x (chunk + warm-up); see DESIGN.md "Tuning".
+ * Automatic chunking: about TARGET_LANES chunks -- two resident 256-lane
+ * workgroups on each of the 256 CUs, whose memory pipelines bound the
+ * speculative kernel.  Uniform chunks of ceil(eblocks / TARGET_LANES)
+ * rounded up to the group measured best (C3: 40 eblocks, 489 workgroups;
+ * C2: 80); an exactly balanced plan of 512 workgroups with two chunk
+ * lengths (XA_VARIANT_BALANCED) was 12 % slower ("Tuning").
  */
-#define TARGET_LANES_STEREO	(256u * 2u * 256u)
-#define TARGET_LANES_MONO	(256u * 4u * 256u)
+#define TARGET_LANES	(256u * 2u * 256u)
+#define XA_VARIANT_STRUCT	0xfu	/* kernel structure, 0 = automatic */
+#define XA_VARIANT_BALANCED	0x20u	/* two-length chunk plan */
 
 static int
 gpu_present(void)
@@ -42,32 +46,70 @@ round_up(uint32_t v, uint32_t m)
 	return (v + m - 1) / m * m;
 }
 
+struct plan {
+	uint32_t	C, W;		/* base chunk and warm-up, eblocks */
+	uint32_t	nlong;		/* leading chunks that are C + G long */
+	uint32_t	nchunks;
+};
+
+/*
+ * Chunk plan for one stream.  Automatic: uniform chunks (above).  With
+ * XA_VARIANT_BALANCED: exactly TARGET_LANES chunks once the stream is long
+ * enough, C = eblocks per lane rounded down to the group (G = 4/ch
+ * eblocks) and the remainder spread as whole groups over the leading
+ * chunks, rounded up to whole waves so every wave has one chunk length.
+ * An explicit tune->chunk gives uniform chunks of that length.
+ */
 static void
-pick_tuning(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
-    uint32_t *C, uint32_t *W)
+plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
+    struct plan *p)
 {
 	const uint32_t G = 4 / ch;
-	uint32_t c = t && t->chunk ? t->chunk : 0;
-	uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup : DEFAULT_WARMUP;
-	if (c == 0) {
-		const uint32_t lanes = ch == 2 ? TARGET_LANES_STEREO :
-		    TARGET_LANES_MONO;
-		c = (eblocks + lanes - 1) / lanes;
-		if (c < 16)
-			c = 16;
+	const uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup :
+	    DEFAULT_WARMUP;
+	uint32_t c;
+	p->W = round_up(w, G);
+	p->nlong = 0;
+	if (t && t->chunk) {
+		c = t->chunk;
+	} else if (!(t && (t->variant & XA_VARIANT_BALANCED))) {
+		c = (uint32_t)(((uint64_t)eblocks + TARGET_LANES - 1) /
+		    TARGET_LANES);
+		if (c < MIN_CHUNK)
+			c = MIN_CHUNK;
+	} else {
+		c = eblocks / TARGET_LANES / G * G;
+		if (c >= MIN_CHUNK) {
+			const uint64_t rest = (uint64_t)eblocks -
+			    (uint64_t)TARGET_LANES * c;
+			const uint32_t nl = round_up((uint32_t)((rest + G - 1) / G),
+			    64u);
+			const uint64_t cover = (uint64_t)nl * (c + G);
+			p->C = c;
+			p->nlong = nl;
+			if (cover >= eblocks)
+				p->nchunks = (uint32_t)((eblocks + c + G - 1) /
+				    (c + G));
+			else
+				p->nchunks = nl + (uint32_t)((eblocks - cover +
+				    c - 1) / c);
+			return;
+		}
+		c = MIN_CHUNK;
 	}
-	*C = round_up(c, G);
-	*W = round_up(w, G);
+	p->C = round_up(c, G);
+	p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
 }
 
-/* kernel structure: bit 1 = non-temporal PCM stores (measured: a small
- * gain for stereo, a loss for mono) */
+/* kernel structure (xa_decode.hip launch()): bit 1 = non-temporal PCM
+ * stores, bits 2-3 = store-phase bytes per lane (measured, DESIGN.md §5:
+ * stereo NT + one eblock = 128 B; mono NT + 128 B) */
 static unsigned
 pick_variant(unsigned ch, const bjxa_hip_tuning_t *t)
 {
-	if (t && t->variant)
-		return t->variant & 0xffu;
-	return ch == 2 ? 2u : 0u;
+	if (t && (t->variant & XA_VARIANT_STRUCT))
+		return t->variant & XA_VARIANT_STRUCT;
+	return ch == 2 ? 2u : 2u | (1u << 2);
 }
 
 static size_t
@@ -80,11 +122,11 @@ extern "C" size_t
 bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
     const bjxa_hip_tuning_t *tune)
 {
-	uint32_t C, W;
+	struct plan p;
 	if (channels != 1 && channels != 2)
 		return 0;
-	pick_tuning(eblocks, channels, tune, &C, &W);
-	return ws_bytes((eblocks + C - 1) / C);
+	plan_chunks(eblocks, channels, tune, &p);
+	return ws_bytes(p.nchunks);
 }
 
 __global__ void
@@ -118,7 +160,7 @@ extern "C" int
 bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
     uint32_t *d_status, const bjxa_hip_tuning_t *tune, void *stream)
 {
-	uint32_t C, W;
+	struct plan p;
 	if (s == NULL || d_ws == NULL || d_status == NULL || s->d_src == NULL ||
 	    s->d_dst == NULL || (s->bits != 4 && s->bits != 6 && s->bits != 8) ||
 	    (s->channels != 1 && s->channels != 2) || s->eblocks == 0 ||
@@ -133,15 +175,16 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 		errno = ENODEV;
 		return -1;
 	}
-	pick_tuning(s->eblocks, s->channels, tune, &C, &W);
+	plan_chunks(s->eblocks, s->channels, tune, &p);
 	xa_dec_args a;
 	a.src = (const uint8_t *)s->d_src;
 	a.dst = (uint8_t *)s->d_dst;
 	a.pcm_bytes = s->frames * 2u * s->channels;
 	a.eblocks = s->eblocks;
-	a.nchunks = (s->eblocks + C - 1) / C;
-	a.C = C;
-	a.W = W;
+	a.nchunks = p.nchunks;
+	a.C = p.C;
+	a.W = p.W;
+	a.nlong = p.nlong;
 	a.init[0] = ((uint32_t)(uint16_t)s->state[0]) |
 	    ((uint32_t)(uint16_t)s->state[1] << 16);
 	a.init[1] = ((uint32_t)(uint16_t)s->state[2]) |

@@ -44,7 +44,10 @@ typedef struct {
 	int32_t		warmup;		/* speculative warm-up eblocks, -1 = auto */
 	void		*ev_spec[2];	/* hipEvent_t pair recorded on `stream`
 					 * around the speculative-decode kernel */
-	uint32_t	variant;	/* kernel structure; 0 = default */
+	uint32_t	variant;	/* bits 0-3: kernel structure, 0 = automatic
+					 * (DESIGN.md §3); bit 5: two-length chunk
+					 * plan.  Pass the same tuning to
+					 * bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 
 /*

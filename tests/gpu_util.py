@@ -12,21 +12,21 @@ def require_gpu():
 
 
 def dev_decode(xa, eblocks, bits, ch, frames=None, state=(0, 0, 0, 0), chunk=0, warmup=-1,
-               want_status=False):
+               want_status=False, variant=0):
     """Decode host XA bytes through bjxa_hip_decode_async; returns int16 PCM."""
     torch = require_gpu()
     if frames is None:
         frames = eblocks * 32
     src = torch.from_numpy(np.ascontiguousarray(xa, dtype=np.uint8)).cuda()
     dst = torch.full((eblocks * 64 * ch,), 0x5A, dtype=torch.uint8, device="cuda")
-    ws_len = bjxa_amd.decode_workspace_size(eblocks, ch, chunk, warmup)
+    ws_len = bjxa_amd.decode_workspace_size(eblocks, ch, chunk, warmup, variant)
     ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
     status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     bjxa_amd.workspace_init(ws.data_ptr(), ws_len, stream)
     bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eblocks, frames, bits, ch,
                            ws.data_ptr(), ws_len, status.data_ptr(), state, chunk, warmup,
-                           stream)
+                           stream, variant=variant)
     torch.cuda.synchronize()
     out = dst.cpu().numpy()
     pcm = out.view(np.int16)[:frames * ch].copy()

@@ -29,3 +29,34 @@ def test_worst_case_mix_full_size(built):
     got, st = dev_decode(xa, eb, 8, 2, want_status=True)
     assert np.array_equal(got, ref)
     assert st[3] > 0      # the repair pass did real work on this mix
+
+
+@pytest.mark.parametrize("bits,ch", [(8, 2), (8, 1), (4, 2), (6, 1)])
+def test_balanced_plan_ragged(built, bits, ch):
+    """The two-length chunk plan (VARIANT_BALANCED) splits a long stream into
+    exactly 512 x 256 chunks (the long ones first, whole waves).  A ragged
+    length, a cut last block and a 2-eblock warm-up (so many chunks need
+    repair across long/short boundaries) must still be bit-exact."""
+    eb = 2_500_003
+    frames = eb * 32 - 7
+    xa = synth.stream(eb, bits, ch, "A", seed=5)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, (1, -2, 3, -4), frames)
+    got, st = dev_decode(xa, eb, bits, ch, frames=frames, state=(1, -2, 3, -4),
+                         warmup=2, want_status=True, variant=bjxa_amd.VARIANT_BALANCED)
+    assert np.array_equal(got, ref)
+    assert st[5] == 131067 and st[3] > 0
+    assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
+
+
+@pytest.mark.parametrize("bits,ch", [(8, 2), (6, 1)])
+def test_auto_plan_ragged(built, bits, ch):
+    """The automatic (uniform) plan on the same ragged stream."""
+    eb = 2_500_003
+    frames = eb * 32 - 7
+    xa = synth.stream(eb, bits, ch, "A", seed=6)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, (5, 6, -7, 8), frames)
+    got, st = dev_decode(xa, eb, bits, ch, frames=frames, state=(5, 6, -7, 8),
+                         want_status=True)
+    assert np.array_equal(got, ref)
+    assert st[6] == 20 and st[5] == -(-eb // 20)
+    assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
