@@ -2,14 +2,17 @@
 """bench.py -- XA ADPCM decode throughput on MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path (bjxa_hip_decode_async: speculative
-decode + verify/repair + tail) over one synthetic XA stream already resident
-in HBM.  Default workload is BASELINE config C3: one 8-bit stereo stream of
-5,000,000 effective blocks (320M int16 samples), profile mix A.
+decode + verify/repair/tail) over one synthetic XA stream already resident
+in HBM.  The bench line is BASELINE config C3 -- one 8-bit stereo stream of
+5,000,000 effective blocks (320M int16 samples), profile mix A -- the case
+north_star quotes its target on; at N=1 the same run also measures C2
+(configs[1]: one 8-bit mono stream of 10,000,000 blocks) and reports it
+under "other_configs".
 
 Multi-GPU (torchrun, one process per GPU): every rank decodes its own
 C3-sized stream (independent objects, no data-path collective), so per-GPU
-work is fixed: "scaling": "weak".  RCCL carries only the barrier and the
-max-over-ranks time.
+work is fixed: "scaling": "weak".  RCCL carries only the barriers, the max
+over ranks of the timed region and the AND of the bit-exact checks.
 
 Reported:
   value       decoded MSamples/s of the whole job (all ranks) over the timed
@@ -17,10 +20,12 @@ Reported:
   roofline    xa_decode_spec, the dominant kernel: algorithmic bytes per
               launch (XA read + PCM written, SURVEY.md §8(d): 3.03125 B per
               8-bit sample) / its mean duration from hipEvents recorded on
-              the launch stream, against 8 TB/s; traffic from the committed
-              rocprofv3 PMC summary (profiles/pmc_latest.json) if present
+              the launch stream, against 8 TB/s; the read-only fraction
+              beside it; traffic = HBM bytes per launch from the committed
+              rocprofv3 PMC summary (profiles/pmc_latest.json)
   cpu_baseline  the oracle (CPU restatement of libbjxa's decode, 1 thread)
-              on the same stream, rank 0 at N=1 only; also the bit-exact check
+              on the same stream, rank 0 at N=1 only: median of 5 passes
+              after a discarded first pass (the bit-exact check)
 """
 import argparse
 import ctypes
@@ -40,6 +45,7 @@ WORKLOADS = {
     "C3": (5_000_000, 8, 2, "C3: 8-bit stereo XA stream, 5,000,000 eblocks"),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+CPU_PASSES = 5
 
 
 def hip_runtime():
@@ -71,33 +77,26 @@ def job_value(samples_per_rank, world, steps, elapsed):
     return samples_per_rank * world * steps / elapsed / 1e6
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
-    ap.add_argument("--mix", default="A", choices=["A", "F", "W", "Z"])
-    ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--warm-blocks", type=int, default=-1)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-verify", action="store_true")
-    args = ap.parse_args()
+def host_cpu():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
+
+def run_workload(name, args, dev, world, rank, verify, cpu_leg):
+    """Decode one seeded stream `args.steps` times (after `args.warmup`
+    untimed steps); returns the measurements of this rank."""
     import torch
     import torch.distributed as dist
     import bjxa_amd
     from bjxa_amd import synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    eb, bits, ch, desc = WORKLOADS[args.workload]
+    eb, bits, ch, desc = WORKLOADS[name]
     samples = eb * 32 * ch
     xa_np = synth.stream(eb, bits, ch, args.mix, seed=rank)
     src = torch.from_numpy(xa_np).to(dev)
@@ -105,8 +104,7 @@ def main():
     ws_len = bjxa_amd.decode_workspace_size(eb, ch, args.chunk, args.warm_blocks)
     ws = torch.zeros(ws_len, dtype=torch.uint8, device=dev)
     status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
+    sh = torch.cuda.current_stream(dev).cuda_stream
     bjxa_amd.workspace_init(ws.data_ptr(), ws_len, sh)
 
     hip = hip_runtime()
@@ -144,56 +142,105 @@ def main():
         hip.hipEventSynchronize(b)
         hip.hipEventElapsedTime(ctypes.byref(ms), a, b)
         spec_ms.append(ms.value)
-    spec_avg_ms = float(np.mean(spec_ms))
-    st = status.cpu().numpy().view(np.uint32)
+    for a, b in evs:
+        hip.hipEventDestroy(a)
+        hip.hipEventDestroy(b)
+    st = status.cpu().numpy().view(np.uint32).copy()
 
-    # bit-exact check of the last step against the oracle
-    ok = None
-    cpu = None
-    if not args.no_verify or (rank == 0 and world == 1 and not args.no_cpu):
+    ok, cpu = None, None
+    if verify or cpu_leg:
         import oracle
         out = dst.cpu().numpy().view(np.int16)
-        t = time.perf_counter()
-        ref, _, _, _ = oracle.decode(xa_np, eb, bits, ch)
-        t_cpu = time.perf_counter() - t
+        ref, _, _, _ = oracle.decode(xa_np, eb, bits, ch)   # also the discarded pass
         ok = bool(np.array_equal(out, ref))
-        del ref
-        if rank == 0 and world == 1 and not args.no_cpu:
-            # two more timed single-thread passes; report the best
-            times = [t_cpu]
-            for _ in range(2):
+        del out
+        if cpu_leg:
+            times = []
+            for _ in range(CPU_PASSES):
                 t = time.perf_counter()
-                oracle.decode(xa_np, eb, bits, ch)
+                oracle.decode(xa_np, eb, bits, ch, out=ref)
                 times.append(time.perf_counter() - t)
-            best = min(times)
-            cpu = {"value": round(samples / best / 1e6, 1), "unit": "MSamples/s", "cores": 1,
+            med = float(np.median(times))
+            cpu = {"value": round(samples / med / 1e6, 1), "unit": "MSamples/s", "cores": 1,
                    "kind": "port",
-                   "sample": "the full %s stream (%d samples), oracle/xa_oracle.c "
-                             "single-pass decode, 1 thread, best of 3" % (args.workload, samples)}
+                   "sample": "the full %s stream (%d samples), oracle/xa_oracle.c single-pass "
+                             "decode on 1 thread, median of %d passes after a discarded first; "
+                             "host CPU: %s" % (name, samples, CPU_PASSES, host_cpu())}
+        del ref
+
+    xa_bytes = eb * ch * (bits * 4 + 1)
+    return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
+            "elapsed": elapsed, "spec_ms": float(np.mean(spec_ms)), "status": st,
+            "xa_bytes": xa_bytes, "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
+
+
+def pmc_traffic(workload, mix):
+    """HBM bytes per spec launch from the committed PMC summary, if it was
+    taken on this workload and mix."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("workload") == workload and d.get("mix") == mix:
+        return d.get("hbm_bytes_per_launch"), d.get("source")
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
+    ap.add_argument("--mix", default="A", choices=["A", "F", "W", "Z"])
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--warm-blocks", type=int, default=-1)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-other", action="store_true", help="skip the C2 line at N=1")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cpu_leg = rank == 0 and world == 1 and not args.no_cpu
+    r = run_workload(args.workload, args, dev, world, rank, not args.no_verify, cpu_leg)
+    elapsed, ok = r["elapsed"], r["ok"]
     if world > 1:
         elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
 
-    xa_bytes = eb * ch * (bits * 4 + 1)
-    pcm_bytes = eb * 64 * ch
-    alg_bytes = xa_bytes + pcm_bytes
-    achieved = alg_bytes / (spec_avg_ms * 1e-3) / 1e9
-    traffic = None
-    traffic_src = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                p = json.load(f)
-            if p.get("workload") == args.workload and p.get("mix") == args.mix:
-                traffic = p.get("hbm_bytes_per_launch")
-                traffic_src = p.get("source")
-        except (OSError, ValueError):
-            traffic = None
+    other = {}
+    if world == 1 and not args.no_other:
+        for name in sorted(WORKLOADS):
+            if name == args.workload:
+                continue
+            o = run_workload(name, args, dev, 1, rank, not args.no_verify, False)
+            other[name] = {
+                "workload": o["desc"], "value": round(job_value(o["samples"], 1, args.steps,
+                                                                o["elapsed"]), 1),
+                "unit": "MSamples/s", "ms_per_step": round(o["elapsed"] / args.steps * 1e3, 4),
+                "spec_ms": round(o["spec_ms"], 4),
+                "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "chunk": int(o["status"][6]), "bit_exact": o["ok"]}
+            ok = ok if o["ok"] in (None, True) else False
 
-    value = job_value(samples, world, args.steps, elapsed)
+    st = r["status"]
+    achieved = r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9
+    read_gbs = r["xa_bytes"] / (r["spec_ms"] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload, args.mix)
     line = {
         "metric": "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs CPU",
-        "value": round(value, 1),
+        "value": round(job_value(r["samples"], world, args.steps, elapsed), 1),
         "unit": "MSamples/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -204,26 +251,27 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (seeded XA stream, profile mix %s, uniform codes)" % args.mix,
-        "config": {"workload": desc + " per rank", "workload_id": args.workload,
-                   "bits": bits, "channels": ch,
-                   "eblocks_per_rank": eb, "samples_per_rank": samples,
+        "config": {"workload": r["desc"] + " per rank", "workload_id": args.workload,
+                   "bits": r["bits"], "channels": r["ch"],
+                   "eblocks_per_rank": r["eb"], "samples_per_rank": r["samples"],
                    "profile_mix": args.mix, "parallelism": "independent streams, 1 per GPU",
                    "chunk": int(st[6]), "warmup_eblocks": int(st[7]),
                    "tuning": "auto" if not args.chunk and args.warm_blocks < 0 else "manual"},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes, "traffic_source": traffic_src,
-                     "launch_ms": round(spec_avg_ms, 4)},
-        "cpu_baseline": cpu,
+                     "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": traffic_src,
+                     "read_only_achieved": round(read_gbs, 1),
+                     "read_only_frac": round(read_gbs / HBM_PEAK_GBS, 4),
+                     "launch_ms": round(r["spec_ms"], 4)},
+        "cpu_baseline": r["cpu"],
         "bit_exact": ok,
         "repaired_chunks": int(st[3]), "tail_repairs": int(st[4]), "chunks": int(st[5]),
     }
+    if other:
+        line["other_configs"] = other
     if rank == 0:
         print(json.dumps(line), flush=True)
-    for a, b in evs:
-        hip.hipEventDestroy(a)
-        hip.hipEventDestroy(b)
     if world > 1:
         dist.destroy_process_group()
     return 0 if ok in (None, True) else 1

@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 cd /tmp
 for W in 0 8 16; do
   timeout -k 10 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --output-format csv \
-      -d "$OUT/w$W" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-verify \
+      -d "$OUT/w$W" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu --no-verify --no-other \
       --chunk 40 --warm-blocks $W "$@" > "$OUT/w$W.log" 2>&1
 done
 echo "calib $TAG done"

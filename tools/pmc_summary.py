@@ -31,8 +31,15 @@ def rows(pattern):
 
 
 def short(name):
+    """Kernel key: name plus <bits,ch> for the templated kernels, so the
+    C3 (8-bit stereo) and C2 (8-bit mono) launches of one run stay apart."""
     for k in ("xa_decode_spec", "xa_decode_fix", "xa_encode_groups", "xa_ws_init"):
         if k in name:
+            i = name.find(k + "<")
+            if i >= 0:
+                inner = name[i + len(k) + 1:name.find(">", i)]
+                args = [x.strip() for x in inner.split(",")]
+                return "%s<%s,%s>" % (k, args[0], args[1])
             return k
     return name[:40]
 
@@ -62,11 +69,13 @@ def main():
     out["pmc"] = counters(os.path.join(d, "pmc[0-9]*", "**", "*counter_collection.csv"))
     w0 = counters(os.path.join(d, "pmc_w0", "**", "*counter_collection.csv"))
     out["pmc_w0"] = w0
-    sp = out["pmc"].get("xa_decode_spec", {})
-    if bench and "TCC_EA0_RDREQ_sum" in sp and "TCC_EA0_RDREQ_sum" in w0.get("xa_decode_spec", {}):
-        cfg = bench["config"]
+    cfg = bench["config"] if bench else None
+    key = "xa_decode_spec<%d,%d>" % (cfg["bits"], cfg["channels"]) if cfg else ""
+    out["spec_key"] = key
+    sp = out["pmc"].get(key, {})
+    if bench and "TCC_EA0_RDREQ_sum" in sp and "TCC_EA0_RDREQ_sum" in w0.get(key, {}):
         xa_bytes = cfg["eblocks_per_rank"] * cfg["channels"] * (cfg["bits"] * 4 + 1)
-        bpr = xa_bytes / w0["xa_decode_spec"]["TCC_EA0_RDREQ_sum"]
+        bpr = xa_bytes / w0[key]["TCC_EA0_RDREQ_sum"]
         read = sp["TCC_EA0_RDREQ_sum"] * bpr
         write = sp.get("WRITE_SIZE", 0.0) * 1024
         t = {"read_bytes": round(read), "write_bytes": round(write),

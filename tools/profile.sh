@@ -23,7 +23,7 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
     -- python3 "$R/bench.py" "$@" > "$OUT/bench.json" 2> "$OUT/trace.log" || {
 	echo "trace pass failed rc=$?"; exit 1; }
-PM="--steps 5 --warmup 1 --no-cpu --no-verify"
+PM="--steps 5 --warmup 1 --no-cpu --no-verify --no-other"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
     "SQ_WAVES SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU" \

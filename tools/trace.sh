@@ -7,5 +7,5 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-    -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --no-verify "$@" > "$OUT/trace.log" 2>&1
+    -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --no-verify --no-other "$@" > "$OUT/trace.log" 2>&1
 echo "trace rc=$?"
