@@ -1,0 +1,59 @@
+"""PCIe-inclusive rate of the unchanged C API: bjxa_decode() on host buffers
+(src/libbjxa.c:602-661 call shape, single pass), through libbjxa.so.0.
+
+The stream is the largest one a single XA header can describe
+(nDataLen < 2^27): 2,000,000 8-bit stereo eblocks or
+4,000,000 8-bit mono blocks.  Reported: MSamples/s and GB/s of host bytes
+moved (XA in + PCM out), median of 5 calls after a discarded first, and the
+check against the oracle.
+
+usage: python tools/host_rate.py [--ch 2|1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+
+import bjxa_amd  # noqa: E402
+from bjxa_amd import synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ch", type=int, default=2)
+    ap.add_argument("--passes", type=int, default=5)
+    args = ap.parse_args()
+    ch = args.ch
+    eb = 2_000_000 if ch == 2 else 4_000_000
+    bits = 8
+    xa = synth.stream(eb, bits, ch, "A", seed=7)
+    hdr = bjxa_amd.xa_header(len(xa), eb * 32, 44100, bits, ch)
+    dst = np.empty(eb * 64 * ch, dtype=np.uint8)
+    times = []
+    with bjxa_amd.Decoder() as d:       # one codec: device buffers persist
+        for i in range(args.passes + 1):
+            d.parse_header(hdr)
+            t = time.perf_counter()
+            n = d.decode(dst, xa)
+            times.append(time.perf_counter() - t)
+            assert n == eb, n
+    import oracle
+    ref, _, _, _ = oracle.decode(xa, eb, bits, ch)
+    ok = bool(np.array_equal(dst.view(np.int16), ref))
+    med = float(np.median(times[1:]))
+    samples = eb * 32 * ch
+    print(json.dumps({"api": "bjxa_decode (host buffers)", "bits": bits, "channels": ch,
+                      "eblocks": eb, "ms": round(med * 1e3, 3),
+                      "MSamples_per_s": round(samples / med / 1e6, 1),
+                      "host_GB_per_s": round((len(xa) + dst.nbytes) / med / 1e9, 2),
+                      "first_call_ms": round(times[0] * 1e3, 3), "bit_exact": ok}))
+
+
+if __name__ == "__main__":
+    main()
