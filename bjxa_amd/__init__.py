@@ -96,6 +96,9 @@ _SIGS = {
     "bjxa_hip_encode_async": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint,
                                              ctypes.c_uint, _P, _P]),
     "bjxa_hip_version": (ctypes.c_char_p, []),
+    "bjxa_hip_batch_new": (ctypes.c_void_p, [_P, ctypes.c_uint32, _P, _P]),
+    "bjxa_hip_batch_decode_async": (ctypes.c_int, [_P, _P, _P, _P]),
+    "bjxa_hip_batch_free": (None, [_P]),
 }
 REFERENCE_SYMBOLS = {  # src/libbjxa.map:16-47
     "LIBBJXA_0.1": ["bjxa_decode", "bjxa_decode_format", "bjxa_decoder", "bjxa_dump_pcm",
@@ -105,9 +108,10 @@ REFERENCE_SYMBOLS = {  # src/libbjxa.map:16-47
                     "bjxa_encode_init", "bjxa_encoder", "bjxa_fread_riff_header",
                     "bjxa_free_encoder", "bjxa_fwrite_header", "bjxa_parse_riff_header"],
 }
-EXTENSION_SYMBOLS = {"LIBBJXA_HIP_0.1": ["bjxa_hip_decode_async", "bjxa_hip_decode_workspace",
-                                         "bjxa_hip_encode_async", "bjxa_hip_version",
-                                         "bjxa_hip_workspace_init"]}
+EXTENSION_SYMBOLS = {"LIBBJXA_HIP_0.1": ["bjxa_hip_batch_decode_async", "bjxa_hip_batch_free",
+                                         "bjxa_hip_batch_new", "bjxa_hip_decode_async",
+                                         "bjxa_hip_decode_workspace", "bjxa_hip_encode_async",
+                                         "bjxa_hip_version", "bjxa_hip_workspace_init"]}
 
 
 def lib():
@@ -296,6 +300,43 @@ def decode_device(d_src, d_dst, eblocks, frames, bits, channels, d_ws, ws_len, d
     t = HipTuning(chunk, warmup, (ctypes.c_void_p * 2)(*events), variant)
     _check(lib().bjxa_hip_decode_async(ctypes.byref(s), d_ws, ws_len, d_status,
                                        ctypes.byref(t), stream), "bjxa_hip_decode_async")
+
+
+class Batch:
+    """bjxa_hip_batch_*: many device-resident streams decoded per launch.
+
+    `streams` is a list of dicts with d_src, d_dst, eblocks, bits, channels
+    and optional frames (default eblocks*32) and state."""
+
+    def __init__(self, streams, chunk=0, warmup=-1, stream=0):
+        arr = (HipStream * len(streams))()
+        for i, d in enumerate(streams):
+            arr[i] = HipStream(d["d_src"], d["d_dst"], d.get("frames", d["eblocks"] * 32),
+                               d["eblocks"], d["bits"], d["channels"],
+                               (ctypes.c_int16 * 4)(*d.get("state", (0, 0, 0, 0))))
+        t = HipTuning(chunk, warmup)
+        self.n = len(streams)
+        self._p = lib().bjxa_hip_batch_new(arr, self.n, ctypes.byref(t), stream)
+        if not self._p:
+            e = ctypes.get_errno()
+            raise BjxaError(e, "bjxa_hip_batch_new: %s" % os.strerror(e))
+
+    def decode(self, d_status, stream=0, events=(None, None)):
+        """Decode every stream; d_status holds n * STATUS_WORDS uint32."""
+        t = HipTuning(0, -1, (ctypes.c_void_p * 2)(*events), 0)
+        _check(lib().bjxa_hip_batch_decode_async(self._p, d_status, ctypes.byref(t), stream),
+               "bjxa_hip_batch_decode_async")
+
+    def close(self):
+        if self._p:
+            lib().bjxa_hip_batch_free(self._p)
+            self._p = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def encode_device(d_pcm, frames, bits, channels, d_xa, stream=0):

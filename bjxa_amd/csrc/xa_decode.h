@@ -45,6 +45,46 @@ struct xa_dec_args {
 hipError_t xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
     unsigned variant, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 
+/*
+ * Batched decode: many independent streams, mixed formats, one launch per
+ * kernel.  Every stream's chunks occupy whole waves of a global chunk index
+ * space (stream i owns global chunks [cbase, cbase + 64 * waves_i)), so
+ * wave w belongs to stream wstream[w] and takes its chunks 64w - cbase ..
+ * +63.
+ */
+struct xa_batch_stream {		/* 64 B, device table entry */
+	const uint8_t *src;
+	uint8_t *dst;
+	uint64_t pcm_bytes;
+	uint32_t eblocks, nchunks;
+	uint32_t cbase;			/* first global chunk, % 64 == 0 */
+	uint32_t C;			/* chunk length, eblocks */
+	uint32_t init[2];
+	uint32_t fmt;			/* bits | channels << 8 */
+	uint32_t pad[3];
+};
+
+/* per-stream control words (xa_batch_args::sctl) */
+#define XA_SCTL_ERR	0
+#define XA_SCTL_FIXED	1
+#define XA_SCTL_TAIL	2
+#define XA_SCTL_WORDS	4
+
+struct xa_batch_args {
+	const xa_batch_stream *streams;
+	const uint32_t *wstream;	/* stream of each wave */
+	uint32_t nstreams, nwaves;	/* global chunks = 64 * nwaves */
+	uint32_t W;
+	uint2 *g, *e;			/* per global chunk */
+	uint32_t *queue;		/* 2 * 64 * nwaves */
+	uint32_t *ctl;			/* XA_CTL_WORDS (NQ, TICKET) */
+	uint32_t *sctl;			/* XA_SCTL_WORDS per stream */
+	uint32_t *status;		/* XA_ST_WORDS per stream */
+};
+
+hipError_t xa_decode_batch_launch(const xa_batch_args &b, hipStream_t st,
+    hipEvent_t ev0, hipEvent_t ev1);
+
 struct xa_enc_args {
 	const uint8_t *src;	/* PCM frames, 16-bit, channels interleaved */
 	uint8_t *dst;		/* XA blocks */

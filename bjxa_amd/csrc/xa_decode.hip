@@ -187,15 +187,15 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
  * wchunk0 + j (whose PCM starts at wstart_b + j * chunk_bytes) and goes to
  * byte `rel_off` of that chunk's PCM.  Lane l
  * stores piece l % P of lines l / P + (64 / P) i (P = LB / 16 pieces per
- * line).  Wave-uniform fast path when every line is whole; otherwise (the
- * grid's last wave only) per-piece bounds and a 2-byte tail for the
- * stream's cut last block.
+ * line).  Wave-uniform fast path when every line is whole; a predicated
+ * copy of it when the stream ends inside the wave on a 16-B boundary;
+ * otherwise (a cut last block) per-piece bounds and a 2-byte tail.
  */
 template <int LB, bool NT>
 __device__ __forceinline__ void
 store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
     uint32_t wchunk0, uint64_t wstart_b, uint32_t chunk_bytes, uint32_t rel_off,
-    bool wave_full, uint8_t *gbase, const uint8_t *lbase)
+    bool wave_full, bool clean, uint8_t *gbase, const uint8_t *lbase)
 {
 	constexpr int LINE = LB + 16, P = LB / 16, LPI = 64 / P;
 #ifdef XA_DBG_NOSTORE
@@ -214,6 +214,26 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 				    (u32x4a *)(gp + i * istride));
 			else
 				*(u32x4a *)(gp + i * istride) = v;
+		}
+		return;
+	}
+	if (clean) {
+		/* the stream ends in this wave but its PCM is a whole number of
+		 * 16-B pieces: the fast path with each piece predicated on lying
+		 * in the stream (pieces of chunks past the end lie beyond it) */
+		uint8_t *gp = gbase + rel_off;
+		const uint8_t *end = a.dst + a.pcm_bytes;
+		const uint64_t istride = (uint64_t)LPI * chunk_bytes;
+#pragma unroll
+		for (int i = 0; i < P; i++) {
+			const u32x4a v = *(const u32x4a *)(lbase + i * LPI * LINE);
+			uint8_t *q = gp + i * istride;
+			if (q + 16 <= end) {
+				if (NT)
+					__builtin_nontemporal_store(v, (u32x4a *)q);
+				else
+					*(u32x4a *)q = v;
+			}
 		}
 		return;
 	}
@@ -318,29 +338,34 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, int64_t wstart,
  *  LB     output line bytes per lane per store phase (64, or the eblock's
  *         64*ch).
  */
+/* per-wave LDS region of K1 */
+template <int BITS, int CH, bool SPLIT, int LB> struct spec_lds {
+	static constexpr int IBUF = 64 * geo<BITS, CH>::SEGB;	/* input */
+	static constexpr int LINE = LB + 16;		/* output line + pad */
+	static constexpr int OBUF = 64 * LINE;		/* output stage */
+	static constexpr int REGION = SPLIT ? IBUF + OBUF :
+	    (IBUF > OBUF ? IBUF : OBUF);
+};
+
+/*
+ * K1 body: one wave decodes chunks wchunk0 .. wchunk0+63 of stream `a`
+ * (wave-uniform), staging through the wave's LDS `region`.
+ */
 template <int BITS, int CH, bool SPLIT, int LB, bool NT>
-__global__ __launch_bounds__(64 * XA_SPEC_WPB) void
-xa_decode_spec(xa_dec_args a)
+__device__ __forceinline__ void
+spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 {
 	typedef geo<BITS, CH> g;
+	typedef spec_lds<BITS, CH, SPLIT, LB> L;
 	constexpr int G = g::G, OB = g::OB, EBSZ = g::EBSZ, GDW = g::GDW;
-	constexpr int IBUF = 64 * g::SEGB;	/* input stage, per wave */
-	constexpr int LINE = LB + 16;		/* output line + pad */
-	constexpr int OBUF = 64 * LINE;		/* output stage, per wave */
-	constexpr int REGION = SPLIT ? IBUF + OBUF : (IBUF > OBUF ? IBUF : OBUF);
+	constexpr int IBUF = L::IBUF, LINE = L::LINE;
 	/* stores issued between a group's DMA and the next group's wait */
 	constexpr int STORES_PER_GROUP = G * OB / 16;
-	__shared__ __attribute__((aligned(16))) uint8_t
-	    lds[XA_SPEC_WPB * REGION];
 
-	/* the wave index is wave-uniform; say so, so that LDS bases and the
-	 * DMA source base live in SGPRs */
 	const int lane = threadIdx.x & 63;
-	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	uint8_t *ibuf = lds + wv * REGION;
+	uint8_t *ibuf = region;
 	uint8_t *obuf = SPLIT ? ibuf + IBUF : ibuf;
 	uint8_t *line = obuf + lane * LINE;
-	const uint32_t wchunk0 = blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u;
 	const uint32_t chunk = wchunk0 + lane;
 	const int64_t eblocks = a.eblocks;
 	/* the wave's chunks are all long or all short (nlong % 64 == 0) */
@@ -405,6 +430,7 @@ xa_decode_spec(xa_dec_args a)
 	const uint64_t full_blocks = a.pcm_bytes / OB;
 	const bool wave_full = wchunk0 + 63u < a.nchunks &&
 	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
+	const bool clean = (a.pcm_bytes & 15u) == 0;
 	bool first = true;
 	for (int s0 = 0; s0 < (int)Cw; s0 += G) {
 		/* this group's DMA, not the previous group's stores */
@@ -428,7 +454,7 @@ xa_decode_spec(xa_dec_args a)
 				wave_lds_sync();
 				store_lines<LB, NT>(a, obuf, lane, wchunk0, wstart_b,
 				    chunk_bytes, (uint32_t)s0 * OB + (uint32_t)LB * h,
-				    wave_full, gbase, lbase);
+				    wave_full, clean, gbase, lbase);
 				wave_lds_sync();
 			};
 			/* every lane runs the decode (flush holds wave-wide
@@ -468,6 +494,21 @@ xa_decode_spec(xa_dec_args a)
 		a.g[chunk] = gv;
 		a.e[chunk] = ev;
 	}
+}
+
+/* K1 for one stream: wave w of the grid takes chunks 64w .. 64w+63 */
+template <int BITS, int CH, bool SPLIT, int LB, bool NT>
+__global__ __launch_bounds__(64 * XA_SPEC_WPB) void
+xa_decode_spec(xa_dec_args a)
+{
+	typedef spec_lds<BITS, CH, SPLIT, LB> L;
+	__shared__ __attribute__((aligned(16))) uint8_t
+	    lds[XA_SPEC_WPB * L::REGION];
+	/* the wave index is wave-uniform; say so, so that LDS bases and the
+	 * DMA source base live in SGPRs */
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	spec_wave<BITS, CH, SPLIT, LB, NT>(a, lds + wv * L::REGION,
+	    blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u);
 }
 
 /* ------------------------------------------------------------------ */
@@ -920,4 +961,270 @@ xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
 	if (bits == 6)
 		return launch<6, 2>(a, variant, st, ev0, ev1);
 	return launch<4, 2>(a, variant, st, ev0, ev1);
+}
+
+/* ------------------------------------------------------------------ */
+/* batched decode: many streams, mixed formats                          */
+
+/* f(BITS, CH) as integral constants for fmt = bits | channels << 8 */
+template <typename F>
+__device__ __forceinline__ void
+with_format(uint32_t fmt, F &&f)
+{
+	typedef std::integral_constant<int, 1> c1;
+	typedef std::integral_constant<int, 2> c2;
+	switch (fmt) {
+	case 8 | 2 << 8:
+		f(std::integral_constant<int, 8>(), c2());
+		break;
+	case 6 | 2 << 8:
+		f(std::integral_constant<int, 6>(), c2());
+		break;
+	case 4 | 2 << 8:
+		f(std::integral_constant<int, 4>(), c2());
+		break;
+	case 8 | 1 << 8:
+		f(std::integral_constant<int, 8>(), c1());
+		break;
+	case 6 | 1 << 8:
+		f(std::integral_constant<int, 6>(), c1());
+		break;
+	default:
+		f(std::integral_constant<int, 4>(), c1());
+		break;
+	}
+}
+
+/* the single-stream argument block of stream `sid` of a batch */
+__device__ __forceinline__ xa_dec_args
+batch_stream_args(const xa_batch_args &b, uint32_t sid)
+{
+	const xa_batch_stream &d = b.streams[sid];
+	xa_dec_args a;
+	a.src = d.src;
+	a.dst = d.dst;
+	a.pcm_bytes = d.pcm_bytes;
+	a.eblocks = d.eblocks;
+	a.nchunks = d.nchunks;
+	a.C = d.C;
+	a.W = b.W;
+	a.nlong = 0;
+	a.init[0] = d.init[0];
+	a.init[1] = d.init[1];
+	a.g = b.g + d.cbase;
+	a.e = b.e + d.cbase;
+	a.queue = b.queue;
+	a.ctl = b.sctl + sid * XA_SCTL_WORDS;	/* [XA_CTL_ERR] == [XA_SCTL_ERR] */
+	a.status = b.status + sid * XA_ST_WORDS;
+	return a;
+}
+
+template <int LB> struct batch_lds {
+	static constexpr int m(int x, int y) { return x > y ? x : y; }
+	static constexpr int REGION = m(m(m(spec_lds<8, 2, false, LB>::REGION,
+	    spec_lds<8, 1, false, LB>::REGION), m(spec_lds<6, 2, false, LB>::REGION,
+	    spec_lds<6, 1, false, LB>::REGION)), m(spec_lds<4, 2, false, LB>::REGION,
+	    spec_lds<4, 1, false, LB>::REGION));
+};
+
+/* K1 over a batch: wave w decodes 64 chunks of stream wstream[w] with that
+ * stream's format (wave-uniform dispatch, no divergence) */
+template <int LB, bool NT>
+__global__ __launch_bounds__(64 * XA_SPEC_WPB) void
+xa_decode_spec_batch(xa_batch_args b)
+{
+	constexpr int R = batch_lds<LB>::REGION;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[XA_SPEC_WPB * R];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const uint32_t w = blockIdx.x * XA_SPEC_WPB + wv;
+	if (w >= b.nwaves)
+		return;
+	const uint32_t sid = __builtin_amdgcn_readfirstlane(b.wstream[w]);
+	const xa_dec_args a = batch_stream_args(b, sid);
+	const uint32_t fmt = __builtin_amdgcn_readfirstlane(b.streams[sid].fmt);
+	const uint32_t wchunk0 = 64u * w -
+	    __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
+	uint8_t *region = lds + wv * R;
+	with_format(fmt, [&](auto bc, auto cc) {
+		spec_wave<decltype(bc)::value, decltype(cc)::value, false, LB, NT>(a,
+		    region, wchunk0);
+	});
+}
+
+/*
+ * Sequential tail of a batch (lanes 0 and 1 of one wave; the heap lives in
+ * lane 0): drain the re-check queue in global chunk order.  Global chunk
+ * indices never cross streams (a stream's chunk 0 is never queued).
+ */
+__device__ static void
+drain_batch(const xa_batch_args &b)
+{
+	const int c = threadIdx.x;
+	const uint32_t nq = b.ctl[XA_CTL_NQ];
+	uint32_t n = 0;
+	if (c == 0)
+		for (uint32_t i = 0; i < nq; i++)
+			heap_push(b.queue, n, b.queue[i]);
+	for (;;) {
+		uint32_t Q = 0;
+		if (c == 0 && n > 0)
+			Q = heap_pop(b.queue, n);
+		Q = __builtin_amdgcn_readfirstlane(Q);
+		if (Q == 0)
+			break;
+		const uint2 s = b.e[Q - 1], gq = b.g[Q];
+		if (s.x == gq.x && s.y == gq.y)
+			continue;
+		const uint32_t sid = b.wstream[Q / 64];
+		const xa_dec_args a = batch_stream_args(b, sid);
+		const uint32_t q = Q - b.streams[sid].cbase;
+		const uint32_t fmt = b.streams[sid].fmt;
+		bool met = false;
+		if (c == 0 || (fmt >> 8) == 2) {
+			uint2 ex;
+			with_format(fmt, [&](auto bc, auto cc) {
+				met = fix_lane<decltype(bc)::value,
+				    decltype(cc)::value>(a, q, c, c ? s.y : s.x, ex);
+			});
+		}
+		if (c == 0) {
+			b.g[Q] = s;
+			b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_TAIL]++;
+			if (!met && q + 1 < a.nchunks)
+				heap_push(b.queue, n, Q + 1);
+		}
+	}
+}
+
+/* K2 over a batch: as xa_decode_fix, over the global chunk space; the last
+ * workgroup also publishes every stream's status */
+__global__ __launch_bounds__(256) void
+xa_decode_fix_batch(xa_batch_args b)
+{
+	constexpr uint32_t SPAN = 256u * XA_FIX_CPT;
+	__shared__ uint32_t last, nfix;
+	__shared__ uint32_t fixq[SPAN];
+	__shared__ uint2 fixs[SPAN];
+	const uint32_t n = 64u * b.nwaves;
+	const uint64_t *e64 = (const uint64_t *)b.e;
+	const uint64_t *g64 = (const uint64_t *)b.g;
+	bool wrote = false;
+	for (uint32_t base = blockIdx.x * SPAN; base < n;
+	    base += gridDim.x * SPAN) {
+		if (threadIdx.x == 0)
+			nfix = 0;
+		__syncthreads();
+		const uint32_t t0 = base + threadIdx.x * XA_FIX_CPT;
+		uint64_t ev[XA_FIX_CPT], gv[XA_FIX_CPT];
+#pragma unroll
+		for (int i = 0; i < XA_FIX_CPT; i++) {
+			const uint32_t Q = min(t0 + i, n - 1);
+			ev[i] = __hip_atomic_load(&e64[Q > 0 ? Q - 1 : 0],
+			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			gv[i] = g64[Q];
+		}
+#pragma unroll
+		for (int i = 0; i < XA_FIX_CPT; i++) {
+			const uint32_t Q = t0 + i;
+			if (Q >= n || ev[i] == gv[i])
+				continue;
+			const xa_batch_stream &d = b.streams[b.wstream[Q / 64]];
+			const uint32_t q = Q - d.cbase;
+			if (q > 0 && q < d.nchunks) {
+				const uint32_t k = atomicAdd(&nfix, 1u);
+				fixq[k] = Q;
+				fixs[k] = make_uint2((uint32_t)ev[i],
+				    (uint32_t)(ev[i] >> 32));
+			}
+		}
+		__syncthreads();
+		const uint32_t nf = nfix;
+		/* a lane pair per chunk (the second idles on mono streams) */
+		const int c = threadIdx.x & 1;
+		for (uint32_t k = threadIdx.x / 2; k < nf; k += 128u) {
+			const uint32_t Q = fixq[k];
+			const uint2 s = fixs[k];
+			const uint32_t sid = b.wstream[Q / 64];
+			const xa_dec_args a = batch_stream_args(b, sid);
+			const uint32_t q = Q - b.streams[sid].cbase;
+			const uint32_t fmt = b.streams[sid].fmt;
+			if (c == 1 && (fmt >> 8) == 1)
+				continue;
+			bool met = false;
+			uint2 ex;
+			with_format(fmt, [&](auto bc, auto cc) {
+				met = fix_lane<decltype(bc)::value,
+				    decltype(cc)::value>(a, q, c, c ? s.y : s.x, ex);
+			});
+			wrote = true;
+			if (c != 0)
+				continue;
+			b.g[Q] = s;
+			atomicAdd(&b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_FIXED], 1u);
+			if (!met && q + 1 < a.nchunks) {
+				uint32_t i = atomicAdd(&b.ctl[XA_CTL_NQ], 1u);
+				b.queue[i] = Q + 1;
+			}
+		}
+		__syncthreads();
+	}
+	/* arrival ticket, as in xa_decode_fix */
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	const int any = __syncthreads_or(wrote);
+	if (threadIdx.x == 0) {
+		if (any) {
+			__threadfence();
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+		last = atomicAdd(&b.ctl[XA_CTL_TICKET], 1u) == gridDim.x - 1;
+	}
+	__syncthreads();
+	if (!last)
+		return;
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	if (threadIdx.x < 2)
+		drain_batch(b);
+	__syncthreads();
+	for (uint32_t sid = threadIdx.x; sid < b.nstreams; sid += 256u) {
+		const xa_batch_stream &d = b.streams[sid];
+		uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
+		uint32_t *st = b.status + sid * XA_ST_WORDS;
+		const uint2 fin = b.e[d.cbase + d.nchunks - 1];
+		st[XA_ST_ERR] = sc[XA_SCTL_ERR];
+		st[XA_ST_STATE_L] = fin.x;
+		st[XA_ST_STATE_R] = fin.y;
+		st[XA_ST_FIXED] = sc[XA_SCTL_FIXED];
+		st[XA_ST_TAIL] = sc[XA_SCTL_TAIL];
+		st[XA_ST_CHUNKS] = d.nchunks;
+		st[XA_ST_C] = d.C;
+		st[XA_ST_W] = b.W;
+		sc[XA_SCTL_ERR] = 0xffffffffu;
+		sc[XA_SCTL_FIXED] = 0;
+		sc[XA_SCTL_TAIL] = 0;
+	}
+	if (threadIdx.x == 0) {
+		b.ctl[XA_CTL_NQ] = 0;
+		b.ctl[XA_CTL_TICKET] = 0;
+	}
+}
+
+hipError_t
+xa_decode_batch_launch(const xa_batch_args &b, hipStream_t st, hipEvent_t ev0,
+    hipEvent_t ev1)
+{
+	const unsigned grid = (b.nwaves + XA_SPEC_WPB - 1) / XA_SPEC_WPB;
+	const uint64_t nch = 64ull * b.nwaves;
+	unsigned grid2 = (unsigned)((nch + 256u * XA_FIX_CPT - 1) /
+	    (256u * XA_FIX_CPT));
+	if (grid2 > 256u)
+		grid2 = 256u;
+	if (ev0 != NULL)
+		(void)hipEventRecord(ev0, st);
+	hipLaunchKernelGGL((xa_decode_spec_batch<128, true>), dim3(grid),
+	    dim3(64 * XA_SPEC_WPB), 0, st, b);
+	if (ev1 != NULL)
+		(void)hipEventRecord(ev1, st);
+	hipLaunchKernelGGL(xa_decode_fix_batch, dim3(grid2), dim3(256), 0, st, b);
+	return hipGetLastError();
 }

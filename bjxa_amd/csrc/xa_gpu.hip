@@ -237,10 +237,212 @@ bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
 	return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* batched decode (bjxa_hip_batch_*)                                    */
+
+struct bjxa_hip_batch {
+	void		*d_ws;
+	xa_batch_args	args;
+};
+
+/* round x up to a multiple of 64 bytes */
+static size_t
+al64(size_t x)
+{
+	return (x + 63) & ~(size_t)63;
+}
+
+__global__ void
+xa_batch_init(uint32_t *ctl, uint32_t *sctl, uint32_t n)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (blockIdx.x == 0 && threadIdx.x < XA_CTL_WORDS)
+		ctl[threadIdx.x] = 0;
+	if (i < n) {
+		sctl[i * XA_SCTL_WORDS + XA_SCTL_ERR] = 0xffffffffu;
+		sctl[i * XA_SCTL_WORDS + XA_SCTL_FIXED] = 0;
+		sctl[i * XA_SCTL_WORDS + XA_SCTL_TAIL] = 0;
+		sctl[i * XA_SCTL_WORDS + 3] = 0;
+	}
+}
+
+static int
+stream_ok(const bjxa_hip_stream_t *s)
+{
+	return s->d_src != NULL && s->d_dst != NULL &&
+	    (s->bits == 4 || s->bits == 6 || s->bits == 8) &&
+	    (s->channels == 1 || s->channels == 2) && s->eblocks != 0 &&
+	    s->frames <= (uint64_t)s->eblocks * 32u &&
+	    s->frames > (uint64_t)(s->eblocks - 1) * 32u &&
+	    ((uintptr_t)s->d_src & 3u) == 0 && ((uintptr_t)s->d_dst & 15u) == 0;
+}
+
+/*
+ * Plan: one budget of channel blocks per lane, Cb = the batch's channel
+ * blocks / TARGET_LANES (at least MIN_CHUNK, a multiple of 4); a stream of
+ * E eblocks and ch channels gets k = round(E*ch / (64*Cb)) >= 1 whole
+ * waves and chunks of ceil(E / 64k) eblocks (rounded up to its group, at
+ * least MIN_CHUNK), so a stereo lane decodes about Cb/2 eblocks and a mono
+ * lane about Cb blocks -- the single-stream optimum (C3: 40, C2: 80).
+ */
+extern "C" bjxa_hip_batch_t *
+bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
+    const bjxa_hip_tuning_t *tune, void *stream)
+{
+	if (s == NULL || n == 0) {
+		errno = EINVAL;
+		return NULL;
+	}
+	uint64_t cblocks = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		if (!stream_ok(&s[i])) {
+			errno = EINVAL;
+			return NULL;
+		}
+		cblocks += (uint64_t)s[i].eblocks * s[i].channels;
+	}
+	if (!gpu_present()) {
+		errno = ENODEV;
+		return NULL;
+	}
+	uint64_t cb = (cblocks + TARGET_LANES - 1) / TARGET_LANES;
+	if (tune && tune->chunk)
+		cb = tune->chunk;
+	if (cb < MIN_CHUNK)
+		cb = MIN_CHUNK;
+	cb = (cb + 3) & ~(uint64_t)3;
+	const uint32_t w = (tune && tune->warmup >= 0) ? (uint32_t)tune->warmup :
+	    DEFAULT_WARMUP;
+
+	xa_batch_stream *hs = (xa_batch_stream *)calloc(n, sizeof *hs);
+	if (hs == NULL) {
+		errno = ENOMEM;
+		return NULL;
+	}
+	uint64_t nwaves = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint32_t E = s[i].eblocks, ch = s[i].channels, G = 4 / ch;
+		uint64_t k = ((uint64_t)E * ch + 32 * cb) / (64 * cb);
+		if (k == 0)
+			k = 1;
+		uint64_t c = (E + 64 * k - 1) / (64 * k);
+		if (c < MIN_CHUNK)
+			c = MIN_CHUNK;
+		c = (c + G - 1) / G * G;
+		const uint32_t nch = (uint32_t)((E + c - 1) / c);
+		hs[i].src = (const uint8_t *)s[i].d_src;
+		hs[i].dst = (uint8_t *)s[i].d_dst;
+		hs[i].pcm_bytes = s[i].frames * 2u * ch;
+		hs[i].eblocks = E;
+		hs[i].nchunks = nch;
+		hs[i].cbase = (uint32_t)(64 * nwaves);
+		hs[i].C = (uint32_t)c;
+		hs[i].init[0] = ((uint32_t)(uint16_t)s[i].state[0]) |
+		    ((uint32_t)(uint16_t)s[i].state[1] << 16);
+		hs[i].init[1] = ((uint32_t)(uint16_t)s[i].state[2]) |
+		    ((uint32_t)(uint16_t)s[i].state[3] << 16);
+		hs[i].fmt = s[i].bits | ch << 8;
+		nwaves += (nch + 63) / 64;
+	}
+	if (64 * nwaves > 0x7fffffffu) {
+		free(hs);
+		errno = EINVAL;
+		return NULL;
+	}
+	uint32_t *hw = (uint32_t *)malloc(nwaves * 4);
+	bjxa_hip_batch_t *b = (bjxa_hip_batch_t *)calloc(1, sizeof *b);
+	if (hw == NULL || b == NULL) {
+		free(hs);
+		free(hw);
+		free(b);
+		errno = ENOMEM;
+		return NULL;
+	}
+	for (uint32_t i = 0, wv = 0; i < n; i++)
+		for (uint32_t j = 0; j < (hs[i].nchunks + 63) / 64; j++)
+			hw[wv++] = i;
+
+	const size_t nc = 64 * nwaves;
+	const size_t o_sctl = al64(XA_CTL_WORDS * 4);
+	const size_t o_str = o_sctl + al64((size_t)n * XA_SCTL_WORDS * 4);
+	const size_t o_wav = o_str + al64((size_t)n * sizeof(xa_batch_stream));
+	const size_t o_g = o_wav + al64(nwaves * 4);
+	const size_t o_e = o_g + nc * 8;
+	const size_t o_q = o_e + nc * 8;
+	const size_t len = o_q + 2 * nc * 4;
+	uint8_t *ws = NULL;
+	if (hipMalloc((void **)&ws, len) != hipSuccess) {
+		free(hs);
+		free(hw);
+		free(b);
+		errno = ENOMEM;
+		return NULL;
+	}
+	b->d_ws = ws;
+	xa_batch_args &a = b->args;
+	a.streams = (const xa_batch_stream *)(ws + o_str);
+	a.wstream = (const uint32_t *)(ws + o_wav);
+	a.nstreams = n;
+	a.nwaves = (uint32_t)nwaves;
+	a.W = (w + 3) & ~3u;
+	a.g = (uint2 *)(ws + o_g);
+	a.e = (uint2 *)(ws + o_e);
+	a.queue = (uint32_t *)(ws + o_q);
+	a.ctl = (uint32_t *)ws;
+	a.sctl = (uint32_t *)(ws + o_sctl);
+	a.status = NULL;
+	int bad = hipMemcpy(ws + o_str, hs, (size_t)n * sizeof *hs,
+	    hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMemcpy(ws + o_wav, hw, nwaves * 4, hipMemcpyHostToDevice) !=
+	    hipSuccess;
+	free(hs);
+	free(hw);
+	if (!bad) {
+		hipLaunchKernelGGL(xa_batch_init, dim3((n + 255) / 256), dim3(256),
+		    0, (hipStream_t)stream, a.ctl, a.sctl, n);
+		bad = hipGetLastError() != hipSuccess;
+	}
+	if (bad) {
+		(void)hipFree(ws);
+		free(b);
+		errno = EIO;
+		return NULL;
+	}
+	return b;
+}
+
+extern "C" int
+bjxa_hip_batch_decode_async(bjxa_hip_batch_t *b, uint32_t *d_status,
+    const bjxa_hip_tuning_t *tune, void *stream)
+{
+	if (b == NULL || d_status == NULL) {
+		errno = EINVAL;
+		return -1;
+	}
+	b->args.status = d_status;
+	if (xa_decode_batch_launch(b->args, (hipStream_t)stream,
+	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
+	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
+		errno = EIO;
+		return -1;
+	}
+	return 0;
+}
+
+extern "C" void
+bjxa_hip_batch_free(bjxa_hip_batch_t *b)
+{
+	if (b == NULL)
+		return;
+	(void)hipDeviceSynchronize();
+	(void)hipFree(b->d_ws);
+	free(b);
+}
+
 extern "C" const char *
 bjxa_hip_version(void)
 {
-	return "bjxa-mi355x 0.1 gfx950 (spec/fix/tail decode, group encode)";
+	return "bjxa-mi355x 0.2 gfx950 (spec/fix decode, batched decode, group encode)";
 }
 
 /* ------------------------------------------------------------------ */

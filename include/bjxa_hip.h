@@ -72,6 +72,24 @@ int bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws,
     size_t ws_len, uint32_t *d_status, const bjxa_hip_tuning_t *tune,
     void *stream);
 
+/*
+ * Batched decode: n independent streams (any mix of bits and channels) in
+ * one launch per kernel -- SURVEY.md §8(d) C4/C5.  bjxa_hip_batch_new
+ * validates the streams, plans chunks, allocates the batch's device
+ * workspace and uploads its tables (the descriptors, including the device
+ * buffers they name, are captured: re-create the batch for other buffers).
+ * Each decode writes n status records of BJXA_HIP_STATUS_WORDS words
+ * (stream i at d_status + 8*i) with the meaning above; tune (optional)
+ * supplies only the profiling events.  Tuning at creation: chunk = channel
+ * blocks per lane (0 = automatic), warmup.
+ */
+typedef struct bjxa_hip_batch bjxa_hip_batch_t;
+bjxa_hip_batch_t *bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
+    const bjxa_hip_tuning_t *tune, void *stream);
+int bjxa_hip_batch_decode_async(bjxa_hip_batch_t *b, uint32_t *d_status,
+    const bjxa_hip_tuning_t *tune, void *stream);
+void bjxa_hip_batch_free(bjxa_hip_batch_t *b);
+
 /* encode `frames` frames of 16-bit PCM into ceil(frames/32) XA eblocks
  * (profile 0, last block zero-padded), d_pcm 16-B aligned, d_xa 4-B */
 int bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,

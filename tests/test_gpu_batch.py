@@ -1,0 +1,113 @@
+"""Batched decode (bjxa_hip_batch_*): many streams of mixed formats per
+launch, each bit-exact against the oracle's single-stream decode
+(src/libbjxa.c:602-661 per stream), with per-stream status."""
+import numpy as np
+import pytest
+
+import bjxa_amd
+import oracle
+from bjxa_amd import synth
+from gpu_util import require_gpu, status_state
+
+pytestmark = pytest.mark.gpu
+
+FORMATS = [(8, 2), (6, 2), (4, 2), (8, 1), (6, 1), (4, 1)]
+
+
+def run_batch(specs, chunk=0, warmup=-1, repeat=1):
+    """specs: list of (xa bytes, eblocks, bits, ch, frames, state).  Returns
+    (pcm list, status array [n, 8])."""
+    torch = require_gpu()
+    srcs, dsts, streams = [], [], []
+    for xa, eb, bits, ch, frames, state in specs:
+        s = torch.from_numpy(np.ascontiguousarray(xa)).cuda()
+        d = torch.full((eb * 64 * ch,), 0x5A, dtype=torch.uint8, device="cuda")
+        srcs.append(s)
+        dsts.append(d)
+        streams.append({"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
+                        "bits": bits, "channels": ch, "frames": frames, "state": state})
+    status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    with bjxa_amd.Batch(streams, chunk, warmup, sh) as b:
+        for _ in range(repeat):
+            b.decode(status.data_ptr(), sh)
+        torch.cuda.synchronize()
+    out = []
+    for (xa, eb, bits, ch, frames, state), d in zip(specs, dsts):
+        raw = d.cpu().numpy()
+        assert (raw[frames * ch * 2:] == 0x5A).all()
+        out.append(raw.view(np.int16)[:frames * ch].copy())
+    return out, status.cpu().numpy().view(np.uint32).reshape(len(specs), -1).copy()
+
+
+def check(specs, pcms, st):
+    for i, ((xa, eb, bits, ch, frames, state), pcm) in enumerate(zip(specs, pcms)):
+        ref, st_ref, done, bad = oracle.decode(xa, eb, bits, ch, state, frames)
+        if bad < 0:
+            assert st[i][0] == bjxa_amd.NO_ERROR, i
+            assert np.array_equal(pcm, ref), "stream %d (%d-bit, %dch, %d eblocks)" % (
+                i, bits, ch, eb)
+            assert status_state(st[i])[:2 * ch] == st_ref[:2 * ch], i
+        else:
+            # first failing channel block; output before it must match
+            assert st[i][0] == done * ch + bad, (i, st[i][0], done, bad)
+            n = done * 32 * ch
+            assert np.array_equal(pcm[:n], ref[:n]), i
+
+
+def make(eb, bits, ch, seed, mix="A", cut=0, state=(0, 0, 0, 0)):
+    xa = synth.stream(eb, bits, ch, mix, seed=seed)
+    return (xa, eb, bits, ch, eb * 32 - cut, state)
+
+
+def test_batch_mixed_formats(built):
+    rng = np.random.default_rng(3)
+    specs = []
+    for i in range(48):
+        bits, ch = FORMATS[i % 6]
+        eb = int(rng.choice([1, 2, 17, 63, 64, 65, 1000, 4097, 20000, 70001]))
+        cut = int(rng.integers(0, 32)) if i % 4 == 0 else 0
+        state = tuple(int(v) for v in rng.integers(-3000, 3000, 4))
+        specs.append(make(eb, bits, ch, 100 + i, cut=cut, state=state))
+    pcms, st = run_batch(specs)
+    check(specs, pcms, st)
+
+
+def test_batch_repairs_and_cascades(built):
+    """Warm-up 0 and short chunks: nearly every chunk is repaired and
+    worst-case profiles cascade through whole chunks."""
+    specs = [make(30000, bits, ch, 200 + i, mix="W" if i % 2 else "A")
+             for i, (bits, ch) in enumerate(FORMATS)]
+    pcms, st = run_batch(specs, chunk=16, warmup=0)
+    check(specs, pcms, st)
+    assert st[:, 3].sum() > 0
+
+
+def test_batch_repeat_reuses_workspace(built):
+    specs = [make(50000, 8, 2, 300), make(50000, 8, 1, 301, cut=5)]
+    pcms, st = run_batch(specs, repeat=3)
+    check(specs, pcms, st)
+
+
+def test_batch_invalid_profiles(built):
+    """A gain nibble >= 5 in some streams reports that stream's first failing
+    channel block; the other streams are unaffected."""
+    specs = []
+    for i, (bits, ch) in enumerate(FORMATS):
+        xa, eb, b_, c_, frames, state = make(5000, bits, ch, 400 + i)
+        if i % 2 == 0:
+            bsz = bits * 4 + 1
+            blk = 1234 * ch + (ch - 1)          # the R block when stereo
+            xa = xa.copy()
+            xa[blk * bsz] = 0x5F
+        specs.append((xa, eb, b_, c_, frames, state))
+    pcms, st = run_batch(specs)
+    check(specs, pcms, st)
+
+
+def test_batch_c5_shape(built):
+    """C5-shaped (8-bit stereo, 65,536 eblocks per stream), 32 streams."""
+    specs = [make(65536, 8, 2, 500 + i) for i in range(32)]
+    pcms, st = run_batch(specs)
+    check(specs, pcms, st)
+    assert (st[:, 6] == 16).all()      # 32 x 131072 channel blocks over 131072 lanes, / 2
