@@ -6,8 +6,9 @@ decode + verify/repair/tail) over one synthetic XA stream already resident
 in HBM.  The bench line is BASELINE config C3 -- one 8-bit stereo stream of
 5,000,000 effective blocks (320M int16 samples), profile mix A -- the case
 north_star quotes its target on; at N=1 the same run also measures C2
-(configs[1]: one 8-bit mono stream of 10,000,000 blocks) and reports it
-under "other_configs".
+(configs[1]: one 8-bit mono stream of 10,000,000 blocks) and the batched
+configs C4 (1024 mixed-format streams per launch) and C5g (one GPU's share of
+C5 at 8 GPUs), reported under "other_configs" (--no-other skips them).
 
 Multi-GPU (torchrun, one process per GPU): every rank decodes its own
 C3-sized stream (independent objects, no data-path collective), so per-GPU
@@ -174,6 +175,86 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
             "xa_bytes": xa_bytes, "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
 
 
+BATCHES = {
+    # C4 = 1024 mixed-format streams; C5 = 1024 8-bit stereo
+    # streams of 65,536 eblocks over 8 GPUs -- "C5g" is one GPU's share
+    "C4": "C4: 1024 streams, bits (4,6,8)[i%3], channels 1+((i/3)&1), 16,384 eblocks each",
+    "C5g": "C5 per-GPU share at 8 GPUs: 128 8-bit stereo streams of 65,536 eblocks",
+}
+
+
+def batch_specs(name, nstreams=0):
+    if name == "C4":
+        n = nstreams or 1024
+        return [((4, 6, 8)[i % 3], 1 + ((i // 3) & 1), 16384) for i in range(n)]
+    return [(8, 2, 65536)] * (nstreams or 128)
+
+
+def run_batch(name, steps, warmup, dev, verify, nstreams=0):
+    """Decode a batch config (bjxa_hip_batch_*: all streams per launch)
+    `steps` times after `warmup` untimed steps."""
+    import torch
+    import bjxa_amd
+    from bjxa_amd import synth
+    specs = batch_specs(name, nstreams)
+    xas, srcs, dsts, streams = [], [], [], []
+    samples = alg = 0
+    for i, (bits, ch, eb) in enumerate(specs):
+        xa = synth.stream(eb, bits, ch, "A", seed=1000 + i)
+        s = torch.from_numpy(xa).to(dev)
+        d = torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
+        xas.append(xa)
+        srcs.append(s)
+        dsts.append(d)
+        streams.append({"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
+                        "bits": bits, "channels": ch})
+        samples += eb * 32 * ch
+        alg += xa.nbytes + eb * 64 * ch
+    status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    hip = hip_runtime()
+    evs = []
+    for _ in range(steps + warmup):
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        hip.hipEventCreate(ctypes.byref(a))
+        hip.hipEventCreate(ctypes.byref(b))
+        evs.append((a.value, b.value))
+    with bjxa_amd.Batch(streams, stream=sh) as batch:
+        for i in range(warmup):
+            batch.decode(status.data_ptr(), sh, evs[i])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(warmup, warmup + steps):
+            batch.decode(status.data_ptr(), sh, evs[i])
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / steps
+    spec = []
+    for a, b in evs[warmup:]:
+        f = ctypes.c_float()
+        hip.hipEventElapsedTime(ctypes.byref(f), a, b)
+        spec.append(f.value)
+    for a, b in evs:
+        hip.hipEventDestroy(a)
+        hip.hipEventDestroy(b)
+    spec_ms = float(np.mean(spec))
+    st = status.cpu().numpy().view(np.uint32).reshape(len(specs), -1)
+    ok = None
+    if verify:
+        import oracle
+        ok = True
+        for (bits, ch, eb), xa, d in zip(specs, xas, dsts):
+            ref, _, _, _ = oracle.decode(xa, eb, bits, ch)
+            if not np.array_equal(d.cpu().numpy().view(np.int16), ref):
+                ok = False
+                break
+    return {"workload": BATCHES.get(name, name), "streams": len(specs),
+            "value": round(samples / dt / 1e6, 1), "unit": "MSamples/s",
+            "ms_per_step": round(dt * 1e3, 4), "spec_ms": round(spec_ms, 4),
+            "frac": round(alg / (spec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "alg_bytes": alg, "repaired": int(st[:, 3].sum()), "tail": int(st[:, 4].sum()),
+            "chunks": int(st[:, 5].sum()), "bit_exact": ok}
+
+
 def pmc_traffic(workload, mix):
     """HBM bytes per spec launch from the committed PMC summary, if it was
     taken on this workload and mix."""
@@ -199,7 +280,8 @@ def main():
     ap.add_argument("--warm-blocks", type=int, default=-1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-other", action="store_true", help="skip the C2 line at N=1")
+    ap.add_argument("--no-other", action="store_true",
+                    help="skip the C2/C4/C5g lines at N=1")
     args = ap.parse_args()
 
     import torch
@@ -233,6 +315,10 @@ def main():
                 "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "chunk": int(o["status"][6]), "bit_exact": o["ok"]}
             ok = ok if o["ok"] in (None, True) else False
+        for name in sorted(BATCHES):
+            o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify)
+            other[name] = o
+            ok = ok if o["bit_exact"] in (None, True) else False
 
     st = r["status"]
     achieved = r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9
