@@ -49,63 +49,109 @@ enc_byte(const uint32_t *pcm, const int p)
 #undef SMP
 }
 
+#define XA_ENC_WPB 4		/* waves per workgroup */
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
+
+__device__ __forceinline__ void
+wave_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int BITS, int CH>
-__global__ __launch_bounds__(256) void
-xa_encode_groups(xa_enc_args a)
+__global__ __launch_bounds__(64 * XA_ENC_WPB) void
+xa_encode_waves(xa_enc_args a)
 {
 	constexpr int BSZ = BITS * 4 + 1, G = 4 / CH, GDW = BSZ;
-	const uint64_t grp = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	constexpr int IN = 64 * 256;		/* PCM bytes per wave */
+	constexpr int NOUT = 64 * GDW * 4;	/* XA bytes per wave */
+	__shared__ __attribute__((aligned(16))) uint8_t lds[XA_ENC_WPB * IN];
+	const int lane = threadIdx.x & 63;
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	uint8_t *buf = lds + wv * IN;
+	const uint64_t grp0 = ((uint64_t)blockIdx.x * XA_ENC_WPB + wv) * 64u;
 	const uint64_t ngroups = ((uint64_t)a.eblocks + G - 1) / G;
-	if (grp >= ngroups)
+	if (grp0 >= ngroups)
 		return;
-	const uint64_t f0 = grp * G * XA_FRAMES;	/* first frame */
+	const uint64_t pcm_bytes = a.frames * CH * 2u;
+	const uint64_t base = grp0 * 256u;		/* wave's first PCM byte */
+	const bool full = base + IN <= pcm_bytes;
+
+	/* stage: DMA instruction i, lane t fills position t % 16 of row
+	 * 4i + t / 16 with piece (t % 16) ^ (row & 15) of that row */
+	const uint64_t lastp = (pcm_bytes - 1) & ~(uint64_t)15;
+#pragma unroll
+	for (int i = 0; i < 16; i++) {
+		const int row = 4 * i + (lane >> 4);
+		const int piece = (lane & 15) ^ (row & 15);
+		uint64_t off = base + (uint64_t)row * 256u + piece * 16u;
+		if (!full && off > lastp)
+			off = lastp;	/* past the end: any valid piece */
+		__builtin_amdgcn_global_load_lds(a.src + off, LDS_PTR(buf + i * 1024),
+		    16, 0, 0);
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	wave_sync();
+
 	uint32_t pcm[64];
-	const uint32_t *sp = (const uint32_t *)(a.src + f0 * CH * 2);
-	if (f0 + G * XA_FRAMES <= a.frames) {
+	const uint8_t *row = buf + lane * 256;
 #pragma unroll
-		for (int i = 0; i < 16; i++) {
-			u32x4a v = ((const u32x4a *)sp)[i];
-			pcm[4 * i] = v.x;
-			pcm[4 * i + 1] = v.y;
-			pcm[4 * i + 2] = v.z;
-			pcm[4 * i + 3] = v.w;
-		}
-	} else {
-		/* last group: frames past the end encode as 0 (:686-690) */
-		const uint64_t nsmp = (a.frames - f0) * CH;
-		const uint16_t *hp = (const uint16_t *)sp;
+	for (int j = 0; j < 16; j++) {
+		const u32x4a v = *(const u32x4a *)(row + 16 * (j ^ (lane & 15)));
+		pcm[4 * j] = v.x;
+		pcm[4 * j + 1] = v.y;
+		pcm[4 * j + 2] = v.z;
+		pcm[4 * j + 3] = v.w;
+	}
+	if (!full) {
+		/* frames past the end encode as 0 (src/libbjxa.c:686-690) */
+		const uint64_t g0 = base + (uint64_t)lane * 256u;
 #pragma unroll
-		for (int i = 0; i < 64; i++) {
-			uint32_t lo = (uint64_t)(2 * i) < nsmp ? hp[2 * i] : 0u;
-			uint32_t hi = (uint64_t)(2 * i + 1) < nsmp ? hp[2 * i + 1] : 0u;
-			pcm[i] = lo | (hi << 16);
+		for (int d = 0; d < 64; d++) {
+			const uint64_t o = g0 + 4u * d;
+			const uint32_t lo = o < pcm_bytes ? 0xffffu : 0u;
+			const uint32_t hi = o + 2u < pcm_bytes ? 0xffff0000u : 0u;
+			pcm[d] &= lo | hi;
 		}
 	}
-	uint32_t out[GDW];
+	wave_sync();
+
+	uint32_t *obuf = (uint32_t *)buf;
 #pragma unroll
-	for (int d = 0; d < GDW; d++) {
-		out[d] = enc_byte<BITS, CH>(pcm, 4 * d) |
+	for (int d = 0; d < GDW; d++)
+		obuf[lane * GDW + d] = enc_byte<BITS, CH>(pcm, 4 * d) |
 		    (enc_byte<BITS, CH>(pcm, 4 * d + 1) << 8) |
 		    (enc_byte<BITS, CH>(pcm, 4 * d + 2) << 16) |
 		    (enc_byte<BITS, CH>(pcm, 4 * d + 3) << 24);
+	wave_sync();
+
+	/* the wave's XA run: groups past the last eblock are not written */
+	const uint64_t nxa = (uint64_t)a.eblocks * CH * BSZ;
+	const uint64_t ostart = grp0 * 4u * BSZ;
+	uint8_t *dst = a.dst + ostart;
+	const uint64_t valid = nxa - ostart < (uint64_t)NOUT ? nxa - ostart :
+	    (uint64_t)NOUT;
+	if (valid == (uint64_t)NOUT && ((uintptr_t)dst & 15u) == 0) {
+#pragma unroll
+		for (int i = 0; i < (NOUT / 16 + 63) / 64; i++) {
+			const int k = 64 * i + lane;
+			if (k < NOUT / 16)
+				__builtin_nontemporal_store(
+				    *(const u32x4a *)(buf + 16 * k),
+				    (u32x4a *)(dst + 16 * k));
+		}
+		return;
 	}
-	/* the group may run past the last eblock: write only real blocks */
-	uint32_t *dp = (uint32_t *)(a.dst + grp * 4 * BSZ);
-	const uint64_t blocks_here = ((uint64_t)a.eblocks - grp * G) < (uint64_t)G ?
-	    ((uint64_t)a.eblocks - grp * G) : (uint64_t)G;
-	if (blocks_here == (uint64_t)G) {
-#pragma unroll
-		for (int d = 0; d < GDW; d++)
-			dp[d] = out[d];
-	} else {
-		const int nbytes = (int)blocks_here * CH * BSZ;
-		uint8_t *bp = (uint8_t *)dp;
-#pragma unroll
-		for (int d = 0; d < GDW; d++)
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				if (4 * d + k < nbytes)
-					bp[4 * d + k] = (uint8_t)(out[d] >> (8 * k));
+	for (uint32_t k = lane; 4u * k < valid; k += 64u) {
+		const uint32_t v = obuf[k];
+		if (4u * k + 4u <= valid) {
+			*(uint32_t *)(dst + 4u * k) = v;
+		} else {
+			for (uint32_t q = 0; 4u * k + q < valid; q++)
+				dst[4u * k + q] = (uint8_t)(v >> (8 * q));
+		}
 	}
 }
 
@@ -115,11 +161,12 @@ xa_encode_launch(const xa_enc_args &a, unsigned bits, unsigned ch,
 {
 	const uint64_t G = 4 / ch;
 	const uint64_t ngroups = ((uint64_t)a.eblocks + G - 1) / G;
-	const unsigned grid = (unsigned)((ngroups + 255) / 256);
+	const uint64_t nwaves = (ngroups + 63) / 64;
+	const unsigned grid = (unsigned)((nwaves + XA_ENC_WPB - 1) / XA_ENC_WPB);
 	if (grid == 0)
 		return hipSuccess;
-#define L(B, C) hipLaunchKernelGGL((xa_encode_groups<B, C>), dim3(grid), \
-    dim3(256), 0, st, a)
+#define L(B, C) hipLaunchKernelGGL((xa_encode_waves<B, C>), dim3(grid), \
+    dim3(64 * XA_ENC_WPB), 0, st, a)
 	if (ch == 1) {
 		if (bits == 8) L(8, 1); else if (bits == 6) L(6, 1); else L(4, 1);
 	} else {
