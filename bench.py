@@ -8,7 +8,8 @@ in HBM.  The bench line is BASELINE config C3 -- one 8-bit stereo stream of
 north_star quotes its target on; at N=1 the same run also measures C2
 (configs[1]: one 8-bit mono stream of 10,000,000 blocks) and the batched
 configs C4 (1024 mixed-format streams per launch) and C5g (one GPU's share of
-C5 at 8 GPUs), reported under "other_configs" (--no-other skips them).
+C5 at 8 GPUs), and the encode direction on C3-shaped PCM, reported under
+"other_configs" (--no-other skips them).
 
 Multi-GPU (torchrun, one process per GPU): every rank decodes its own
 C3-sized stream (independent objects, no data-path collective), so per-GPU
@@ -255,6 +256,43 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0):
             "chunks": int(st[:, 5].sum()), "bit_exact": ok}
 
 
+def run_encode(steps, warmup, dev, verify):
+    """bjxa_hip_encode_async on C3-shaped PCM (5,000,000 8-bit stereo
+    eblocks = 320M samples), the GPU side of bjxa_encode()."""
+    import torch
+    import bjxa_amd
+    from bjxa_amd import synth
+    eb, bits, ch = 5_000_000, 8, 2
+    frames = eb * 32
+    pcm = synth.pcm(frames, ch, seed=3)
+    src = torch.from_numpy(pcm).to(dev)
+    nxa = eb * ch * (bits * 4 + 1)
+    dst = torch.empty(nxa, dtype=torch.uint8, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warmup):
+        bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    ms = e0.elapsed_time(e1) / steps
+    ok = None
+    if verify:
+        import oracle
+        ok = bool(np.array_equal(dst.cpu().numpy(), oracle.encode(pcm, frames, bits, ch)))
+    alg = pcm.nbytes + nxa
+    return {"workload": "encode, C3-shaped: 320M int16 samples (8-bit stereo) -> XA",
+            "value": round(frames * ch / dt / 1e6, 1), "unit": "MSamples/s",
+            "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ms, 4),
+            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
+            "byte_exact": ok}
+
+
 def pmc_traffic(workload, mix):
     """HBM bytes per spec launch from the committed PMC summary, if it was
     taken on this workload and mix."""
@@ -319,6 +357,9 @@ def main():
             o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify)
             other[name] = o
             ok = ok if o["bit_exact"] in (None, True) else False
+        o = run_encode(args.steps, args.warmup, dev, not args.no_verify)
+        other["encode_C3"] = o
+        ok = ok if o["byte_exact"] in (None, True) else False
 
     st = r["status"]
     achieved = r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9
