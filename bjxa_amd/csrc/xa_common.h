@@ -59,27 +59,8 @@ xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
 	p0 = t;
 	return t;
 #endif
-#ifdef XA_STEP_SHORT
-	/*
-	 * Shorter dependency chain: t*256 + p1*K1 is ready one step early
-	 * (p1 is the previous step's p0), so g2 = p0*K0 + that runs beside
-	 * g = p0*K0 + p1*K1, and floor((g2 + bias) / 256) = t + trunc(g/256)
-	 * because t*256 is a multiple of 256.  Chain: mad, ashr, add, ashr,
-	 * med3 (5 instead of 6).  The empty asm keeps the compiler from
-	 * re-deriving g2 as g + t*256 on the chain.
-	 */
-	int32_t c1 = __mul24(p1, k1);
-	int32_t c2 = c1 + (t << 8);
-	int32_t k0b = k0;
-	asm("" : "+v"(k0b), "+v"(c1), "+v"(c2));
-	int32_t g = __mul24(p0, k0) + c1;
-	int32_t g2 = __mul24(p0, k0b) + c2;
-	asm("" : "+v"(g2));
-	int32_t s = (g2 + (int32_t)((uint32_t)(g >> 31) >> 24)) >> 8;
-#else
 	int32_t g = __mul24(p0, k0) + __mul24(p1, k1);
 	int32_t s = t + ((g + (int32_t)((uint32_t)(g >> 31) >> 24)) >> 8);
-#endif
 	s = min(max(s, -32768), 32767);
 	p1 = p0;
 	p0 = s;

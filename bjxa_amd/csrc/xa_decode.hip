@@ -204,6 +204,23 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 		return;
 #endif
 	if (wave_full) {
+#ifdef XA_DBG_CONTIG
+		/* diagnostic build only (wrong layout): the same bytes, each
+		 * store instruction writing 1 KiB contiguously inside the
+		 * wave's own region */
+		{
+			uint8_t *wp = a.dst + wstart_b + (uint64_t)rel_off * 64u +
+			    (uint64_t)lane * 16u;
+#pragma unroll
+			for (int i = 0; i < P; i++) {
+				const u32x4a v = *(const u32x4a *)(lbase +
+				    i * LPI * LINE);
+				__builtin_nontemporal_store(v,
+				    (u32x4a *)(wp + i * 1024));
+			}
+			return;
+		}
+#endif
 		uint8_t *gp = gbase + rel_off;
 		const uint64_t istride = (uint64_t)LPI * chunk_bytes;
 #pragma unroll
@@ -331,40 +348,38 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, int64_t wstart,
 
 /*
  * K1.  One lane per chunk, XA_SPEC_WPB waves per workgroup.
- *  SPLIT  separate input and output LDS regions: the next group's DMA is
- *         issued before the decode and waited for with a counted vmcnt that
- *         leaves the group's stores in flight.  Otherwise one region serves
- *         both and the DMA follows the group's last store phase.
- *  LB     output line bytes per lane per store phase (64, or the eblock's
- *         64*ch).
+ *  LB  output bytes per lane per store phase (64, 128 or 256; a phase may
+ *      span eblocks)
+ *  NT  non-temporal PCM stores
+ * One LDS region per wave serves both directions: a group's input is
+ * copied to VGPRs, then its output lines are staged and stored, then the
+ * next group's DMA is issued.  (Separate regions with the DMA issued before
+ * the decode and a counted vmcnt measured no faster)
  */
 /* per-wave LDS region of K1 */
-template <int BITS, int CH, bool SPLIT, int LB> struct spec_lds {
+template <int BITS, int CH, int LB> struct spec_lds {
 	static constexpr int IBUF = 64 * geo<BITS, CH>::SEGB;	/* input */
 	static constexpr int LINE = LB + 16;		/* output line + pad */
 	static constexpr int OBUF = 64 * LINE;		/* output stage */
-	static constexpr int REGION = SPLIT ? IBUF + OBUF :
-	    (IBUF > OBUF ? IBUF : OBUF);
+	static constexpr int REGION = IBUF > OBUF ? IBUF : OBUF;
 };
 
 /*
  * K1 body: one wave decodes chunks wchunk0 .. wchunk0+63 of stream `a`
  * (wave-uniform), staging through the wave's LDS `region`.
  */
-template <int BITS, int CH, bool SPLIT, int LB, bool NT>
+template <int BITS, int CH, int LB, bool NT>
 __device__ __forceinline__ void
 spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 {
 	typedef geo<BITS, CH> g;
-	typedef spec_lds<BITS, CH, SPLIT, LB> L;
+	typedef spec_lds<BITS, CH, LB> L;
 	constexpr int G = g::G, OB = g::OB, EBSZ = g::EBSZ, GDW = g::GDW;
-	constexpr int IBUF = L::IBUF, LINE = L::LINE;
-	/* stores issued between a group's DMA and the next group's wait */
-	constexpr int STORES_PER_GROUP = G * OB / 16;
+	constexpr int LINE = L::LINE;
 
 	const int lane = threadIdx.x & 63;
 	uint8_t *ibuf = region;
-	uint8_t *obuf = SPLIT ? ibuf + IBUF : ibuf;
+	uint8_t *obuf = ibuf;
 	uint8_t *line = obuf + lane * LINE;
 	const uint32_t chunk = wchunk0 + lane;
 	const int64_t eblocks = a.eblocks;
@@ -431,21 +446,12 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 	const bool wave_full = wchunk0 + 63u < a.nchunks &&
 	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
 	const bool clean = (a.pcm_bytes & 15u) == 0;
-	bool first = true;
 	for (int s0 = 0; s0 < (int)Cw; s0 += G) {
-		/* this group's DMA, not the previous group's stores */
-		if (!SPLIT || first || !wave_full)
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		else
-			asm volatile("s_waitcnt vmcnt(%0)" :: "n"(STORES_PER_GROUP)
-			    : "memory");
-		first = false;
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
 		for (int i = 0; i < GDW; i++)
 			w[i] = mine[i];
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-		if (SPLIT && s0 + G < (int)Cw)
-			stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, s0 + G, voff);
 		auto body = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
 			const int s = s0 + u;
@@ -480,7 +486,7 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 			}
 		};
 		sfor<0, G>::run(body);
-		if (!SPLIT && s0 + G < (int)Cw) {
+		if (s0 + G < (int)Cw) {
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, s0 + G, voff);
 		}
@@ -497,17 +503,17 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 }
 
 /* K1 for one stream: wave w of the grid takes chunks 64w .. 64w+63 */
-template <int BITS, int CH, bool SPLIT, int LB, bool NT>
+template <int BITS, int CH, int LB, bool NT>
 __global__ __launch_bounds__(64 * XA_SPEC_WPB) void
 xa_decode_spec(xa_dec_args a)
 {
-	typedef spec_lds<BITS, CH, SPLIT, LB> L;
+	typedef spec_lds<BITS, CH, LB> L;
 	__shared__ __attribute__((aligned(16))) uint8_t
 	    lds[XA_SPEC_WPB * L::REGION];
 	/* the wave index is wave-uniform; say so, so that LDS bases and the
 	 * DMA source base live in SGPRs */
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	spec_wave<BITS, CH, SPLIT, LB, NT>(a, lds + wv * L::REGION,
+	spec_wave<BITS, CH, LB, NT>(a, lds + wv * L::REGION,
 	    blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u);
 }
 
@@ -919,9 +925,8 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
 	/* variant bit 1: non-temporal PCM stores; bits 2-3: bytes per lane
-	 * per store phase (0: one eblock, 1: 128, 2: 256).  (SPLIT staging
-	 * regions measured no gain and are not instantiated.) */
-#define SPEC(LB, NT) hipLaunchKernelGGL((xa_decode_spec<BITS, CH, false, LB, NT>), \
+	 * per store phase (0: one eblock, 1: 128, 2: 256) */
+#define SPEC(LB, NT) hipLaunchKernelGGL((xa_decode_spec<BITS, CH, LB, NT>), \
     dim3(grid), dim3(per), 0, st, a)
 	const bool nt = (variant & 2u) != 0;
 	switch ((variant >> 2) & 3u) {
@@ -938,7 +943,7 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 #undef SPEC
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
-#if !defined(XA_DBG_STEP) && !defined(XA_DBG_NOSTORE)
+#if !defined(XA_DBG_STEP) && !defined(XA_DBG_NOSTORE) && !defined(XA_DBG_CONTIG)
 	hipLaunchKernelGGL((xa_decode_fix<BITS, CH>), dim3(grid2), dim3(256), 0,
 	    st, a);
 #endif
@@ -1021,10 +1026,10 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 
 template <int LB> struct batch_lds {
 	static constexpr int m(int x, int y) { return x > y ? x : y; }
-	static constexpr int REGION = m(m(m(spec_lds<8, 2, false, LB>::REGION,
-	    spec_lds<8, 1, false, LB>::REGION), m(spec_lds<6, 2, false, LB>::REGION,
-	    spec_lds<6, 1, false, LB>::REGION)), m(spec_lds<4, 2, false, LB>::REGION,
-	    spec_lds<4, 1, false, LB>::REGION));
+	static constexpr int REGION = m(m(m(spec_lds<8, 2, LB>::REGION,
+	    spec_lds<8, 1, LB>::REGION), m(spec_lds<6, 2, LB>::REGION,
+	    spec_lds<6, 1, LB>::REGION)), m(spec_lds<4, 2, LB>::REGION,
+	    spec_lds<4, 1, LB>::REGION));
 };
 
 /* K1 over a batch: wave w decodes 64 chunks of stream wstream[w] with that
@@ -1046,7 +1051,7 @@ xa_decode_spec_batch(xa_batch_args b)
 	    __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
 	uint8_t *region = lds + wv * R;
 	with_format(fmt, [&](auto bc, auto cc) {
-		spec_wave<decltype(bc)::value, decltype(cc)::value, false, LB, NT>(a,
+		spec_wave<decltype(bc)::value, decltype(cc)::value, LB, NT>(a,
 		    region, wchunk0);
 	});
 }

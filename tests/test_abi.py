@@ -5,6 +5,7 @@ declare them, bjxa_format_t keeps its layout, and the errno contract holds
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -121,3 +122,34 @@ def test_riff_roundtrip(built, golden):
     assert fmt == {"data_len_pcm": 2646000, "blocks": 0, "block_size_pcm": 0,
                    "block_size_xa": 0, "samples_rate": 44100, "sample_bits": 16,
                    "channels": 2}
+
+
+BATCH_PROBE = r"""
+import errno, sys
+sys.path.insert(0, sys.argv[1])
+import bjxa_amd
+def err(streams):
+    try:
+        bjxa_amd.Batch(streams)
+    except bjxa_amd.BjxaError as e:
+        return e.errno
+    return 0
+ok = {"d_src": 0x10000, "d_dst": 0x20000, "eblocks": 100, "bits": 8, "channels": 2}
+res = [err([]), err([dict(ok, bits=5)]), err([dict(ok, channels=3)]),
+       err([dict(ok, d_dst=0x20008)]), err([dict(ok, d_src=0x10002)]),
+       err([dict(ok, frames=100 * 32 + 1)]), err([dict(ok, frames=99 * 32)]),
+       err([ok, dict(ok, eblocks=0)]), err([ok, dict(ok, bits=4, channels=1)])]
+print(" ".join(str(r) for r in res))
+"""
+
+
+def test_batch_argument_checks(built):
+    """bjxa_hip_batch_new validates every descriptor (EINVAL) before it
+    needs the device (ENODEV without one)."""
+    import errno
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    r = subprocess.run([sys.executable, "-c", BATCH_PROBE, ROOT], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = [int(v) for v in r.stdout.split()]
+    assert got == [errno.EINVAL] * 8 + [errno.ENODEV], got
