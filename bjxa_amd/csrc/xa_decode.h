@@ -85,6 +85,21 @@ struct xa_batch_args {
 hipError_t xa_decode_batch_launch(const xa_batch_args &b, hipStream_t st,
     hipEvent_t ev0, hipEvent_t ev1);
 
+/*
+ * Low-latency path for small host-API calls (xa_small.hip): input, PCM and
+ * status in one pinned, device-mapped host buffer per codec.
+ */
+#define XA_SMALL_MAX	32	/* eblocks per call */
+#define XA_SMALL_IN	4096	/* input area (XA or PCM) */
+#define XA_SMALL_STATUS	4096	/* status words, offset within the output area */
+#define XA_SMALL_BYTES	(XA_SMALL_IN + XA_SMALL_STATUS + 64)
+
+hipError_t xa_small_decode_launch(const uint8_t *in_h, uint8_t *out_h,
+    uint32_t n, unsigned bits, unsigned ch, const uint32_t init[2],
+    hipStream_t st);
+hipError_t xa_small_encode_launch(const uint8_t *in_h, uint8_t *out_h,
+    uint64_t frames, unsigned bits, unsigned ch, hipStream_t st);
+
 struct xa_enc_args {
 	const uint8_t *src;	/* PCM frames, 16-bit, channels interleaved */
 	uint8_t *dst;		/* XA blocks */

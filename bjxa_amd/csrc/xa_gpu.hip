@@ -452,6 +452,8 @@ struct bjxa__gpu {
 	hipStream_t	stream;
 	void		*d_in, *d_out, *d_ws;
 	size_t		in_cap, out_cap, ws_cap;
+	uint8_t		*h_small;	/* pinned: small-call in | out | status */
+	uint8_t		*d_small;	/* its device view */
 	uint32_t	*d_status;
 };
 
@@ -505,6 +507,8 @@ bjxa__gpu_free(struct bjxa__gpu *g)
 	(void)hipFree(g->d_out);
 	(void)hipFree(g->d_ws);
 	(void)hipFree(g->d_status);
+	if (g->h_small != NULL)
+		(void)hipHostFree(g->h_small);
 	(void)hipStreamDestroy(g->stream);
 	free(g);
 }
@@ -516,11 +520,69 @@ io_fail(void)
 	return -1;
 }
 
+static int
+small_buffer(struct bjxa__gpu *g)
+{
+	if (g->h_small != NULL)
+		return 0;
+	if (hipHostMalloc((void **)&g->h_small, XA_SMALL_BYTES,
+	    hipHostMallocDefault) != hipSuccess) {
+		g->h_small = NULL;
+		errno = ENOMEM;
+		return -1;
+	}
+	if (hipHostGetDevicePointer((void **)&g->d_small, g->h_small, 0) !=
+	    hipSuccess) {
+		(void)hipHostFree(g->h_small);
+		g->h_small = NULL;
+		errno = EIO;
+		return -1;
+	}
+	return 0;
+}
+
+/* at most XA_SMALL_MAX eblocks: one launch over the pinned buffer */
+static int
+small_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
+    unsigned bits, unsigned ch, int16_t state[4], void *dst,
+    uint64_t dst_bytes, uint32_t *err_cb)
+{
+	const size_t in_bytes = (size_t)(bits * 4 + 1) * ch * eblocks;
+	uint32_t init[2];
+
+	if (small_buffer(g) < 0)
+		return -1;
+	memcpy(g->h_small, src, in_bytes);
+	init[0] = ((uint32_t)(uint16_t)state[0]) |
+	    ((uint32_t)(uint16_t)state[1] << 16);
+	init[1] = ((uint32_t)(uint16_t)state[2]) |
+	    ((uint32_t)(uint16_t)state[3] << 16);
+	if (xa_small_decode_launch(g->d_small, g->d_small + XA_SMALL_IN, eblocks,
+	    bits, ch, init, g->stream) != hipSuccess ||
+	    hipStreamSynchronize(g->stream) != hipSuccess)
+		return io_fail();
+	const volatile uint32_t *st = (const volatile uint32_t *)(g->h_small +
+	    XA_SMALL_IN + XA_SMALL_STATUS);
+	*err_cb = st[0];
+	if (st[0] != 0xffffffffu && dst_bytes > (uint64_t)(st[0] / ch) * 64u * ch)
+		dst_bytes = (uint64_t)(st[0] / ch) * 64u * ch;
+	state[0] = (int16_t)(st[1] & 0xffffu);
+	state[1] = (int16_t)(st[1] >> 16);
+	state[2] = (int16_t)(st[2] & 0xffffu);
+	state[3] = (int16_t)(st[2] >> 16);
+	memcpy(dst, g->h_small + XA_SMALL_IN, dst_bytes);
+	return 0;
+}
+
 extern "C" int
 bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
     unsigned bits, unsigned ch, int16_t state[4], void *dst,
     uint64_t dst_bytes, uint32_t *err_cb)
 {
+	if (eblocks <= XA_SMALL_MAX)
+		return small_decode(g, src, eblocks, bits, ch, state, dst,
+		    dst_bytes, err_cb);
+
 	const size_t ebsz = (size_t)(bits * 4 + 1) * ch;
 	const size_t in_bytes = ebsz * eblocks;
 	const size_t out_full = (size_t)eblocks * 64u * ch;
@@ -601,6 +663,19 @@ bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
 	const size_t in_bytes = (size_t)frames * 2u * ch;
 	const uint32_t eblocks = (uint32_t)((frames + 31) / 32);
 	const size_t out_bytes = (size_t)eblocks * (bits * 4 + 1) * ch;
+
+	if (eblocks <= XA_SMALL_MAX) {
+		/* one launch over the pinned buffer */
+		if (small_buffer(g) < 0)
+			return -1;
+		memcpy(g->h_small, src, in_bytes);
+		if (xa_small_encode_launch(g->d_small, g->d_small + XA_SMALL_IN,
+		    frames, bits, ch, g->stream) != hipSuccess ||
+		    hipStreamSynchronize(g->stream) != hipSuccess)
+			return io_fail();
+		memcpy(dst, g->h_small + XA_SMALL_IN, out_bytes);
+		return 0;
+	}
 
 	if (grow(&g->d_in, &g->in_cap, in_bytes + 256) < 0 ||
 	    grow(&g->d_out, &g->out_cap, out_bytes + 256) < 0)
