@@ -22,7 +22,8 @@ Reported:
   roofline    xa_decode_spec, the dominant kernel: algorithmic bytes per
               launch (XA read + PCM written, SURVEY.md §8(d): 3.03125 B per
               8-bit sample) / its mean duration from hipEvents recorded on
-              the launch stream, against 8 TB/s; the read-only fraction
+              the launch stream (every EV_EVERY-th timed step), against
+              8 TB/s; the read-only fraction
               beside it; traffic = HBM bytes per launch from the committed
               rocprofv3 PMC summary (profiles/pmc_latest.json)
   cpu_baseline  the oracle (CPU restatement of libbjxa's decode, 1 thread)
@@ -48,6 +49,10 @@ WORKLOADS = {
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 CPU_PASSES = 5
+# hipEvent pairs around the spec kernel are recorded on every EV_EVERY-th
+# timed step only: a timing event drains the stream (measured +5.5 us per
+# step when recorded on every step)
+EV_EVERY = 5
 
 
 def hip_runtime():
@@ -119,9 +124,10 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
         evs.append((a.value, b.value))
 
     def step(i):
+        ev = evs[i] if (i - args.warmup) % EV_EVERY == 0 else (None, None)
         bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, bits, ch,
                                ws.data_ptr(), ws_len, status.data_ptr(), (0, 0, 0, 0),
-                               args.chunk, args.warm_blocks, sh, evs[i])
+                               args.chunk, args.warm_blocks, sh, ev)
 
     for i in range(args.warmup):
         step(i)
@@ -139,7 +145,10 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     elapsed = t1 - t0
 
     spec_ms = []
-    for a, b in evs[args.warmup:]:
+    for i in range(args.warmup, nev):
+        if (i - args.warmup) % EV_EVERY:
+            continue
+        a, b = evs[i]
         ms = ctypes.c_float()
         hip.hipEventSynchronize(b)
         hip.hipEventElapsedTime(ctypes.byref(ms), a, b)
@@ -226,11 +235,15 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(warmup, warmup + steps):
-            batch.decode(status.data_ptr(), sh, evs[i])
+            batch.decode(status.data_ptr(), sh,
+                         evs[i] if (i - warmup) % EV_EVERY == 0 else (None, None))
         torch.cuda.synchronize(dev)
         dt = (time.perf_counter() - t0) / steps
     spec = []
-    for a, b in evs[warmup:]:
+    for i in range(warmup, warmup + steps):
+        if (i - warmup) % EV_EVERY:
+            continue
+        a, b = evs[i]
         f = ctypes.c_float()
         hip.hipEventElapsedTime(ctypes.byref(f), a, b)
         spec.append(f.value)
@@ -310,8 +323,8 @@ def pmc_traffic(workload, mix):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--mix", default="A", choices=["A", "F", "W", "Z"])
     ap.add_argument("--chunk", type=int, default=0)
