@@ -190,6 +190,7 @@ BATCHES = {
     # streams of 65,536 eblocks over 8 GPUs -- "C5g" is one GPU's share
     "C4": "C4: 1024 streams, bits (4,6,8)[i%3], channels 1+((i/3)&1), 16,384 eblocks each",
     "C5g": "C5 per-GPU share at 8 GPUs: 128 8-bit stereo streams of 65,536 eblocks",
+    "C5": "C5: 1024 8-bit stereo streams of 65,536 eblocks, a contiguous share per rank",
 }
 
 
@@ -197,19 +198,32 @@ def batch_specs(name, nstreams=0):
     if name == "C4":
         n = nstreams or 1024
         return [((4, 6, 8)[i % 3], 1 + ((i // 3) & 1), 16384) for i in range(n)]
+    if name == "C5":
+        return [(8, 2, 65536)] * (nstreams or 1024)
     return [(8, 2, 65536)] * (nstreams or 128)
 
 
-def run_batch(name, steps, warmup, dev, verify, nstreams=0):
+def shard_range(n, rank, world):
+    """Contiguous share [lo, hi) of n streams for `rank` of `world`."""
+    return rank * n // world, (rank + 1) * n // world
+
+
+def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1):
     """Decode a batch config (bjxa_hip_batch_*: all streams per launch)
-    `steps` times after `warmup` untimed steps."""
+    `steps` times after `warmup` untimed steps.  With world > 1 this rank
+    takes a contiguous share of the streams (seeded by global index, so the
+    job is the same at every N) and the timed region is bracketed by
+    barriers."""
     import torch
+    import torch.distributed as dist
     import bjxa_amd
     from bjxa_amd import synth
     specs = batch_specs(name, nstreams)
+    lo, hi = shard_range(len(specs), rank, world)
     xas, srcs, dsts, streams = [], [], [], []
     samples = alg = 0
-    for i, (bits, ch, eb) in enumerate(specs):
+    for i in range(lo, hi):
+        bits, ch, eb = specs[i]
         xa = synth.stream(eb, bits, ch, "A", seed=1000 + i)
         s = torch.from_numpy(xa).to(dev)
         d = torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
@@ -220,6 +234,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0):
                         "bits": bits, "channels": ch})
         samples += eb * 32 * ch
         alg += xa.nbytes + eb * 64 * ch
+    specs = specs[lo:hi]
     status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
     hip = hip_runtime()
@@ -233,12 +248,18 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0):
         for i in range(warmup):
             batch.decode(status.data_ptr(), sh, evs[i])
         torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(warmup, warmup + steps):
             batch.decode(status.data_ptr(), sh,
                          evs[i] if (i - warmup) % EV_EVERY == 0 else (None, None))
         torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t0) / steps
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        dt = elapsed / steps
     spec = []
     for i in range(warmup, warmup + steps):
         if (i - warmup) % EV_EVERY:
@@ -262,6 +283,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0):
                 ok = False
                 break
     return {"workload": BATCHES.get(name, name), "streams": len(specs),
+            "samples": samples, "elapsed": elapsed,
             "value": round(samples / dt / 1e6, 1), "unit": "MSamples/s",
             "ms_per_step": round(dt * 1e3, 4), "spec_ms": round(spec_ms, 4),
             "frac": round(alg / (spec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -325,7 +347,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS) + ["C5"],
+                    help="C3/C2: one stream per rank (weak scaling); C5: 1024 "
+                         "streams split over the ranks (strong scaling)")
     ap.add_argument("--mix", default="A", choices=["A", "F", "W", "Z"])
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--warm-blocks", type=int, default=-1)
@@ -345,6 +369,9 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+
+    if args.workload == "C5":
+        return main_c5(args, dev, world, rank)
 
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu
     r = run_workload(args.workload, args, dev, world, rank, not args.no_verify, cpu_leg)
@@ -410,6 +437,39 @@ def main():
     }
     if other:
         line["other_configs"] = other
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok in (None, True) else 1
+
+
+def main_c5(args, dev, world, rank):
+    """C5: the fixed job of 1024 8-bit stereo streams (65,536 eblocks each)
+    split over the ranks -- strong scaling, no data-path collective."""
+    import torch.distributed as dist
+    r = run_batch("C5", args.steps, args.warmup, dev, not args.no_verify, 0, rank, world)
+    elapsed, ok = r["elapsed"], r["bit_exact"]
+    if world > 1:
+        elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
+    total = 1024 * 65536 * 64
+    line = {
+        "metric": "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs CPU",
+        "value": round(total * args.steps / elapsed / 1e6, 1), "unit": "MSamples/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (seeded XA streams, profile mix A, uniform codes)",
+        "config": {"workload": BATCHES["C5"], "workload_id": "C5",
+                   "streams_per_rank": r["streams"],
+                   "parallelism": "stream shards, one batched launch per GPU"},
+        "roofline": {"bound": "hbm", "kernel": "xa_decode_spec_batch (rank 0)",
+                     "achieved": round(r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["frac"],
+                     "traffic": None, "alg_bytes_per_launch": r["alg_bytes"],
+                     "launch_ms": r["spec_ms"]},
+        "cpu_baseline": None, "bit_exact": ok,
+    }
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

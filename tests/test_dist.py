@@ -73,3 +73,17 @@ def test_job_value_weak_scaling():
     assert bench.job_value(320_000_000, 2, 20, 0.01) == pytest.approx(1.28e6)
     # per-GPU work fixed: doubling ranks at equal time doubles the value
     assert bench.job_value(1, 4, 1, 1.0) == 2 * bench.job_value(1, 2, 1, 1.0)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_c5_shards_cover_the_job(world):
+    """bench.py --workload C5: the ranks' contiguous shares of the 1024
+    streams are disjoint, cover them all, and differ by at most one."""
+    import bench
+    n = len(bench.batch_specs("C5"))
+    assert n == 1024
+    got = [bench.shard_range(n, r, world) for r in range(world)]
+    assert got[0][0] == 0 and got[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+    sizes = [hi - lo for lo, hi in got]
+    assert max(sizes) - min(sizes) <= 1
