@@ -87,3 +87,67 @@ def test_c5_shards_cover_the_job(world):
     assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
     sizes = [hi - lo for lo, hi in got]
     assert max(sizes) - min(sizes) <= 1
+
+
+def _split_worker(rank, world, port, q, eb, bits, ch, mix, warmup, frames, init):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from bjxa_amd import dist as bdist, synth
+        xa = synth.stream(eb, bits, ch, mix, seed=77)
+        ebsz = (bits * 4 + 1) * ch
+        lo, hi = bdist.split_ranges(eb, world)[rank]
+        out = {}
+        calls = []
+
+        def local_decode(first, state):
+            calls.append(first)
+            st = state
+            if first < lo:
+                _, st, _, _ = oracle.decode(xa[first * ebsz:lo * ebsz].copy(), lo - first,
+                                            bits, ch, state)
+            fr = min(frames, hi * 32) - lo * 32
+            pcm, ex, _, _ = oracle.decode(xa[lo * ebsz:hi * ebsz].copy(), hi - lo, bits, ch,
+                                          st, fr)
+            out["pcm"] = pcm
+            return st, ex
+
+        fin = bdist.resolve(local_decode, lo, hi, init, warmup)
+        q.put((rank, out["pcm"].tobytes(), fin, len(calls)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,eb,bits,ch,mix,warmup", [
+    (2, 3000, 8, 2, "A", 8), (3, 3001, 6, 1, "W", 2), (3, 4000, 4, 2, "W", 0),
+    (3, 10, 8, 2, "A", 8)])
+def test_single_stream_split(world, eb, bits, ch, mix, warmup):
+    """bjxa_amd.dist.resolve: a stream split over ranks, each decoding its
+    range speculatively (warm-up from (0,0)) and re-decoding when the
+    all-gathered chain of states says its entry was wrong, equals the
+    single-pass decode; ranges shorter than the warm-up start at eblock 0."""
+    import oracle
+    from bjxa_amd import synth
+    frames = eb * 32 - 5
+    init = (11, -22, 33, -44) if ch == 2 else (11, -22, 0, 0)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q, eb, bits, ch, mix,
+                                                       warmup, frames, init))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    xa = synth.stream(eb, bits, ch, mix, seed=77)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, init, frames)
+    assert b"".join(r[1] for r in res) == ref.tobytes()
+    for r in res:
+        assert tuple(r[2])[:2 * ch] == tuple(st_ref)[:2 * ch]
+    if mix == "W" and eb > 100:
+        assert any(r[3] > 1 for r in res)      # some rank had to re-decode
