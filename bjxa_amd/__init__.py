@@ -99,6 +99,7 @@ _SIGS = {
     "bjxa_hip_batch_new": (ctypes.c_void_p, [_P, ctypes.c_uint32, _P, _P]),
     "bjxa_hip_batch_decode_async": (ctypes.c_int, [_P, _P, _P, _P]),
     "bjxa_hip_batch_free": (None, [_P]),
+    "bjxa_hip_decode_files": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint32]),
 }
 REFERENCE_SYMBOLS = {  # src/libbjxa.map:16-47
     "LIBBJXA_0.1": ["bjxa_decode", "bjxa_decode_format", "bjxa_decoder", "bjxa_dump_pcm",
@@ -110,6 +111,7 @@ REFERENCE_SYMBOLS = {  # src/libbjxa.map:16-47
 }
 EXTENSION_SYMBOLS = {"LIBBJXA_HIP_0.1": ["bjxa_hip_batch_decode_async", "bjxa_hip_batch_free",
                                          "bjxa_hip_batch_new", "bjxa_hip_decode_async",
+                                         "bjxa_hip_decode_files",
                                          "bjxa_hip_decode_workspace", "bjxa_hip_encode_async",
                                          "bjxa_hip_version", "bjxa_hip_workspace_init"]}
 
@@ -337,6 +339,45 @@ class Batch:
 
     def __exit__(self, *a):
         self.close()
+
+
+def decode_files(files):
+    """bjxa_hip_decode_files: XA files (bytes) -> [(WAV bytes, errno)].
+
+    Every WAV buffer is sized from its header (44 + data_len_pcm); a file
+    whose header does not parse gets b"" and its errno."""
+    n = len(files)
+    bufs = [ctypes.create_string_buffer(bytes(f), len(f)) for f in files]
+    outs = []
+    for f in files:
+        size = 44
+        h = parse_header_fields(f)
+        if h is not None and h["bits"] in (4, 6, 8) and h["channels"] in (1, 2):
+            # bounded by what the file can hold, whatever the header says
+            data_len = min(h["data_len"], max(len(f) - 32, 0))
+            most = 32 * data_len // ((h["bits"] * 4 + 1) * h["channels"])
+            size += min(h["samples"], most) * h["channels"] * 2
+        outs.append(ctypes.create_string_buffer(size))
+    xa = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+    xl = (ctypes.c_size_t * n)(*[len(f) for f in files])
+    wv = (ctypes.c_void_p * n)(*[ctypes.addressof(o) for o in outs])
+    wl = (ctypes.c_size_t * n)(*[len(o) for o in outs])
+    st = (ctypes.c_int * n)()
+    _check(lib().bjxa_hip_decode_files(xa, xl, wv, wl, st, n), "bjxa_hip_decode_files")
+    res = []
+    for o, f, s in zip(outs, files, st):
+        h = parse_header_fields(f)
+        res.append((o.raw if h is not None else b"", int(s)))
+    return res
+
+
+def parse_header_fields(data):
+    """Raw XA header fields (src/libbjxa.c:409-421), no validation."""
+    if len(data) < 32 or bytes(data[:4]) != b"KWD1":
+        return None
+    data_len, samples, rate, bits, ch = struct.unpack("<IIHBB", bytes(data[4:16]))
+    return {"data_len": data_len, "samples": samples, "rate": rate, "bits": bits,
+            "channels": ch}
 
 
 def encode_device(d_pcm, frames, bits, channels, d_xa, stream=0):

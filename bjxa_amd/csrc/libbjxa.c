@@ -20,6 +20,7 @@
 #include <sys/types.h>
 
 #include "bjxa.h"
+#include "bjxa_hip.h"
 #include "xa_gpu.h"
 
 #define XA_FRAMES	32
@@ -559,4 +560,100 @@ bjxa_encode(bjxa_encoder_t *enc, void *dst, size_t dst_len, const void *src,
 	f->blocks -= (uint32_t)n;
 	f->data_len_pcm -= (uint32_t)take;
 	return ((int)n);
+}
+
+/* ---- many files in one batched pass (LIBBJXA_HIP_0.1) ----------------- */
+
+/*
+ * bjxa_hip_decode_files: decode n complete XA files (32-byte header +
+ * blocks) held in host memory into n complete WAV files -- the 44-byte RIFF
+ * header of bjxa_dump_riff_header followed by the PCM (host order, which
+ * is little-endian on the hosts this library targets, so bjxa_dump_pcm's
+ * conversion is the identity) -- with one batched GPU pass over all of
+ * them.  status[i] is 0 or the errno file i failed with: EPROTO for a bad
+ * header or a block profile with gain >= 5 (the WAV then holds the header
+ * and the PCM before that block), ENOBUFS for an input shorter than its
+ * header announces or an output smaller than 44 + data_len_pcm.  Returns
+ * the number of files decoded completely, or -1 with errno (EFAULT,
+ * EINVAL, or the device's ENODEV/ENOMEM/EIO) when the batch itself fails.
+ */
+int
+bjxa_hip_decode_files(const void *const *xa, const size_t *xa_len,
+    void *const *wav, const size_t *wav_len, int *status, uint32_t n)
+{
+	struct bjxa__job *jobs;
+	uint32_t *which, nj = 0;
+	int done = 0;
+
+	NEED_PTR(xa);
+	NEED_PTR(xa_len);
+	NEED_PTR(wav);
+	NEED_PTR(wav_len);
+	NEED_PTR(status);
+	REQUIRE(n > 0, EINVAL);
+	jobs = calloc(n, sizeof *jobs);
+	which = calloc(n, sizeof *which);
+	if (jobs == NULL || which == NULL) {
+		free(jobs);
+		free(which);
+		FAIL(ENOMEM);
+	}
+	for (uint32_t i = 0; i < n; i++) {
+		const uint8_t *h = xa[i];
+		bjxa_decoder_t d;
+		bjxa_format_t f;
+
+		status[i] = 0;
+		if (h == NULL || wav[i] == NULL) {
+			status[i] = EFAULT;
+			continue;
+		}
+		if (xa_len[i] < BJXA_HEADER_SIZE_XA) {
+			status[i] = ENOBUFS;
+			continue;
+		}
+		/* a stereo payload of an odd number of channel blocks would
+		 * trip the format assertion (:597): refuse it here instead */
+		if (h[15] == 2 && (h[14] == 4 || h[14] == 6 || h[14] == 8) &&
+		    get_le(h + 4, 4) % (2u * (h[14] * 4u + 1u)) != 0) {
+			status[i] = EPROTO;
+			continue;
+		}
+		memset(&d, 0, sizeof d);
+		d.magic = DEC_MAGIC;
+		if (bjxa_parse_header(&d, h, xa_len[i]) < 0) {
+			status[i] = errno;
+			continue;
+		}
+		dec_format(&d, &f);
+		if (xa_len[i] < BJXA_HEADER_SIZE_XA + (size_t)f.blocks *
+		    f.block_size_xa || wav_len[i] < BJXA_HEADER_SIZE_RIFF +
+		    (size_t)f.data_len_pcm) {
+			status[i] = ENOBUFS;
+			continue;
+		}
+		(void)bjxa_dump_riff_header(&d, wav[i], BJXA_HEADER_SIZE_RIFF);
+		jobs[nj].src = h + BJXA_HEADER_SIZE_XA;
+		jobs[nj].dst = (uint8_t *)wav[i] + BJXA_HEADER_SIZE_RIFF;
+		jobs[nj].dst_bytes = f.data_len_pcm;
+		jobs[nj].eblocks = f.blocks;
+		jobs[nj].bits = d.bits;
+		jobs[nj].ch = d.channels;
+		memcpy(jobs[nj].state, d.state, sizeof d.state);
+		which[nj++] = i;
+	}
+	if (nj > 0 && bjxa__gpu_decode_many(jobs, nj) < 0) {
+		const int e = errno;
+		free(jobs);
+		free(which);
+		FAIL(e);
+	}
+	for (uint32_t k = 0; k < nj; k++)
+		if (jobs[k].err_cb != 0xffffffffu)
+			status[which[k]] = EPROTO;
+	for (uint32_t i = 0; i < n; i++)
+		done += status[i] == 0;
+	free(jobs);
+	free(which);
+	return (done);
 }

@@ -29,6 +29,24 @@ int bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
     unsigned bits, unsigned ch, int16_t state[4], void *dst,
     uint64_t dst_bytes, uint32_t *err_cb);
 
+/* one stream of a many-file decode (bjxa_hip_decode_files) */
+struct bjxa__job {
+	const void	*src;		/* host XA blocks */
+	void		*dst;		/* host PCM destination */
+	uint64_t	dst_bytes;	/* PCM bytes wanted (the last block may be cut) */
+	uint32_t	eblocks;
+	uint8_t		bits, ch;
+	int16_t		state[4];
+	uint32_t	err_cb;		/* out: as bjxa__gpu_decode */
+};
+
+/*
+ * Decode n independent streams from host memory in one batched pass
+ * (bjxa_hip_batch_*); each job's PCM lands in its dst, up to the first
+ * failing eblock.  Returns 0 or -1/errno (ENODEV, ENOMEM, EIO).
+ */
+int bjxa__gpu_decode_many(struct bjxa__job *jobs, uint32_t n);
+
 /* encode `frames` frames from host `src` into ceil(frames/32) eblocks */
 int bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
     unsigned bits, unsigned ch, void *dst);

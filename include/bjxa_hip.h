@@ -90,6 +90,18 @@ int bjxa_hip_batch_decode_async(bjxa_hip_batch_t *b, uint32_t *d_status,
     const bjxa_hip_tuning_t *tune, void *stream);
 void bjxa_hip_batch_free(bjxa_hip_batch_t *b);
 
+/*
+ * Decode n complete XA files (32-byte header + blocks) held in host memory
+ * into n complete WAV files (44-byte RIFF header + PCM) with one batched
+ * GPU pass.  wav[i] needs 44 + data_len_pcm bytes.  status[i]: 0, EPROTO
+ * (bad header, or a block profile with gain >= 5: the WAV then holds the
+ * PCM before it), ENOBUFS (input shorter than announced, output too small)
+ * or EFAULT.  Returns the number of files decoded completely, or -1 with
+ * errno if the batch itself fails.
+ */
+int bjxa_hip_decode_files(const void *const *xa, const size_t *xa_len,
+    void *const *wav, const size_t *wav_len, int *status, uint32_t n);
+
 /* encode `frames` frames of 16-bit PCM into ceil(frames/32) XA eblocks
  * (profile 0, last block zero-padded), d_pcm 16-B aligned, d_xa 4-B */
 int bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
