@@ -68,6 +68,71 @@ xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
 }
 
 /*
+ * Both channels of one stereo frame in one instruction stream, on the
+ * packed-f32 pipe (the two chains ride the two halves of v_pk_fma_f32):
+ *
+ *   g    = p0 * K0/256 + p1 * K1/256          v_pk_mul_f32 + v_pk_fma_f32
+ *   q    = trunc(g)                           v_cvt_i32_f32 x2
+ *   s    = q + t                              v_add_u32_sdwa (sext t) x2
+ *   out  = sat16(s) packed L | R << 16        v_cvt_pk_i16_i32
+ *   p0'  = float(out.lo), float(out.hi)       v_cvt_f32_i32_sdwa x2
+ *
+ * Exactness: p0, p1 are int16 and |K0| <= 488, |K1| <= 240, so each product
+ * is exact in f32 (|p*K| < 2^24) and the fma rounds once; the sum is exact
+ * while |g*256| < 2^24.  Beyond that |q| >= 65536 both before and after
+ * rounding, so s saturates to the same int16 either way.  v_cvt_i32_f32
+ * truncates toward zero, which is the reference's `/ 256` on int
+ * (src/libbjxa.c:565-566), and v_cvt_pk_i16_i32 saturates as its clamp
+ * (:567-570).
+ *
+ * `t` holds the two int16 inflate values already shifted by range (low half
+ * L, high half R).  Returns the frame; p0/p1 advance.
+ */
+typedef float xa_f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t
+xa_step_lr(uint32_t t, xa_f2 k0, xa_f2 k1, xa_f2 &p0, xa_f2 &p1)
+{
+#if defined(XA_DBG_STEP)
+	(void)k0;
+	(void)k1;
+	p1 = p0;
+	return t;
+#endif
+	const xa_f2 g = __builtin_elementwise_fma(p0, k0, p1 * k1);
+	const int32_t sl = (int32_t)g.x + (int32_t)(int16_t)(t & 0xffffu);
+	const int32_t sr = (int32_t)g.y + (int32_t)(int16_t)(t >> 16);
+	typedef short xa_s2 __attribute__((ext_vector_type(2)));
+	const xa_s2 pk = __builtin_amdgcn_cvt_pk_i16(sl, sr);
+	const uint32_t fr = __builtin_bit_cast(uint32_t, pk);
+	const float fl = (float)(int16_t)(fr & 0xffffu);
+	const float fh = (float)(int16_t)(fr >> 16);
+	p1 = p0;
+	p0 = xa_f2{fl, fh};
+	return fr;
+}
+
+/* per-channel K pair of a gain as the f32 factors of xa_step_lr */
+__device__ __forceinline__ void
+xa_gain_f(uint32_t gain, float &k0, float &k1)
+{
+	int32_t a, b;
+	xa_gain(gain, a, b);
+	k0 = (float)a * (1.0f / 256.0f);
+	k1 = (float)b * (1.0f / 256.0f);
+}
+
+/* two int16 values shifted right arithmetically, each by its own count
+ * (v_pk_ashrrev_i16: low half by sh's low half, high by its high half) */
+__device__ __forceinline__ uint32_t
+xa_pk_ashr(uint32_t v, uint32_t sh)
+{
+	uint32_t r;
+	asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(r) : "v"(sh), "v"(v));
+	return r;
+}
+
+/*
  * The helpers below take byte/code indices as plain ints: every call site
  * sits inside fully unrolled loops, so the indices fold to constants and
  * w[] stays in VGPRs (checked: no scratch in the kernel resource usage).

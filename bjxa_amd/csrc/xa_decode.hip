@@ -54,6 +54,9 @@
 #ifndef XA_DMA_AUX
 #define XA_DMA_AUX 0		/* cache policy bits of the input LDS-DMA */
 #endif
+#ifndef XA_STEREO_LR
+#define XA_STEREO_LR 1		/* stereo K1 on the packed-f32 step */
+#endif
 
 /* ------------------------------------------------------------------ */
 
@@ -142,13 +145,39 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		xa_gain(gain & 7u, k0[c], k1[c]);
 		bad |= (gain >= 5u) ? (1u << c) : 0u;
 	}
+	/* stereo: both chains in one packed-f32 instruction stream
+	 * (xa_step_lr); the int state converts in and out once per eblock */
+	xa_f2 f0 = {0.f, 0.f}, f1 = {0.f, 0.f}, fk0 = {0.f, 0.f}, fk1 = {0.f, 0.f};
+	uint32_t shp = 0;
+	if (CH == 2) {
+		f0 = xa_f2{(float)p0[0], (float)p0[CH - 1]};
+		f1 = xa_f2{(float)p1[0], (float)p1[CH - 1]};
+		fk0 = xa_f2{(float)k0[0], (float)k0[CH - 1]} * (1.0f / 256.0f);
+		fk1 = xa_f2{(float)k1[0], (float)k1[CH - 1]} * (1.0f / 256.0f);
+		shp = (sh[0] - 16u) | ((sh[CH - 1] - 16u) << 16);
+	}
 	/* 16-B piece q holds 4 stereo frames or 8 mono samples */
 #pragma unroll
 	for (int q = 0; q < 4 * CH; q++) {
 		uint32_t fr[4];
 #pragma unroll
 		for (int j = 0; j < 4; j++) {
-			if (CH == 2) {
+			if (CH == 2 && XA_STEREO_LR) {
+				const int n = 4 * q + j;
+				uint32_t tp;
+				if (BITS == 8) {
+					/* code n of L -> bits 8..15, of R -> 24..31 */
+					const int bl = O + 1 + n, br = O + BSZ + 1 + n;
+					tp = __builtin_amdgcn_perm(w[br >> 2], w[bl >> 2],
+					    0x000c000cu | (uint32_t)(bl & 3) << 8 |
+					    (uint32_t)(4 + (br & 3)) << 24);
+				} else {
+					tp = __builtin_amdgcn_perm(
+					    (uint32_t)code_at<BITS>(w, O + BSZ, n),
+					    (uint32_t)code_at<BITS>(w, O, n), 0x07060302u);
+				}
+				fr[j] = xa_step_lr(xa_pk_ashr(tp, shp), fk0, fk1, f0, f1);
+			} else if (CH == 2) {
 				const int n = 4 * q + j;
 				int32_t sl = xa_step(code_at<BITS>(w, O, n), sh[0],
 				    k0[0], k1[0], p0[0], p1[0]);
@@ -178,6 +207,12 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		/* keep the unpack of later codes from being hoisted here: it
 		 * would only raise register pressure */
 		__builtin_amdgcn_sched_barrier(0);
+	}
+	if (CH == 2 && XA_STEREO_LR) {
+		p0[0] = (int32_t)f0.x;
+		p0[CH - 1] = (int32_t)f0.y;
+		p1[0] = (int32_t)f1.x;
+		p1[CH - 1] = (int32_t)f1.y;
 	}
 	return bad;
 }
@@ -366,9 +401,16 @@ template <int BITS, int CH, int LB> struct spec_lds {
 
 /*
  * K1 body: one wave decodes chunks wchunk0 .. wchunk0+63 of stream `a`
- * (wave-uniform), staging through the wave's LDS `region`.
+ * (wave-uniform), staging through the wave's two LDS buffers `region` and
+ * `region + RS`.  In the chunk phase they alternate: group s is copied out
+ * of buffer s&1 into VGPRs, group s+1's DMA is issued into the other buffer
+ * at once, and group s's output lines are staged in buffer s&1 (free after
+ * the copy).  So the DMA lands while the group decodes, and the wait for it
+ * (vmcnt(XA_NST): all but the group's own 16 stores, which count in issue
+ * order) leaves the stores in flight.
  */
-template <int BITS, int CH, int LB, bool NT>
+#define XA_NST 16	/* store instructions per group (G * OB / 16) */
+template <int BITS, int CH, int LB, bool NT, int RS>
 __device__ __forceinline__ void
 spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 {
@@ -378,9 +420,9 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 	constexpr int LINE = L::LINE;
 
 	const int lane = threadIdx.x & 63;
+	static_assert(G * OB / 16 == XA_NST, "store count per group");
+	static_assert(RS >= L::REGION, "buffer stride");
 	uint8_t *ibuf = region;
-	uint8_t *obuf = ibuf;
-	uint8_t *line = obuf + lane * LINE;
 	const uint32_t chunk = wchunk0 + lane;
 	const int64_t eblocks = a.eblocks;
 	/* the wave's chunks are all long or all short (nlong % 64 == 0) */
@@ -410,6 +452,7 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 
 	uint32_t w[GDW];
 	const uint32_t *mine = (const uint32_t *)(ibuf + lane * g::SEGB);
+	uint8_t *line = ibuf + lane * LINE;
 	auto none = [](int) {};
 	stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, -W, voff);
 
@@ -440,18 +483,33 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 	constexpr int P = LB / 16;
 	uint8_t *gbase = a.dst + wstart_b + (uint64_t)(lane / P) * chunk_bytes +
 	    (lane % P) * 16;
-	const uint8_t *lbase = obuf + (lane / P) * LINE + (lane % P) * 16;
+	const uint32_t lofs = (lane / P) * LINE + (lane % P) * 16;
 	/* every line of this wave lies before the stream's first cut block */
 	const uint64_t full_blocks = a.pcm_bytes / OB;
 	const bool wave_full = wchunk0 + 63u < a.nchunks &&
 	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
 	const bool clean = (a.pcm_bytes & 15u) == 0;
+	int cur = 0;	/* buffer holding the group about to be decoded */
 	for (int s0 = 0; s0 < (int)Cw; s0 += G) {
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		uint8_t *cb = region + (cur ? RS : 0), *ob = region + (cur ? 0 : RS);
+#ifndef XA_DBG_NOSTORE
+		/* the group's DMA is older than the previous group's XA_NST
+		 * stores (fast path only; the edge paths store per piece) */
+		if (s0 != 0 && wave_full)
+			asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA_NST) : "memory");
+		else
+#endif
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		mine = (const uint32_t *)(cb + lane * g::SEGB);
+		line = cb + lane * LINE;
+		const uint8_t *obuf = cb, *lbase = cb + lofs;
 #pragma unroll
 		for (int i = 0; i < GDW; i++)
 			w[i] = mine[i];
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		if (s0 + G < (int)Cw)
+			stage_group<BITS, CH>(a, ob, lane, wstart, Cw, s0 + G, voff);
+		asm volatile("" ::: "memory");
 		auto body = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
 			const int s = s0 + u;
@@ -486,10 +544,9 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 			}
 		};
 		sfor<0, G>::run(body);
-		if (s0 + G < (int)Cw) {
-			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-			stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, s0 + G, voff);
-		}
+		/* the staged lines have been read back (the stores hold VGPRs) */
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		cur ^= 1;
 	}
 	if (chunk < a.nchunks) {
 		uint2 gv, ev;
@@ -509,11 +566,11 @@ xa_decode_spec(xa_dec_args a)
 {
 	typedef spec_lds<BITS, CH, LB> L;
 	__shared__ __attribute__((aligned(16))) uint8_t
-	    lds[XA_SPEC_WPB * L::REGION];
+	    lds[XA_SPEC_WPB * 2 * L::REGION];
 	/* the wave index is wave-uniform; say so, so that LDS bases and the
 	 * DMA source base live in SGPRs */
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	spec_wave<BITS, CH, LB, NT>(a, lds + wv * L::REGION,
+	spec_wave<BITS, CH, LB, NT, L::REGION>(a, lds + wv * 2 * L::REGION,
 	    blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u);
 }
 
@@ -925,16 +982,14 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
 	/* variant bit 1: non-temporal PCM stores; bits 2-3: bytes per lane
-	 * per store phase (0: one eblock, 1: 128, 2: 256) */
+	 * per store phase (0: one eblock, 1: 128; 256-B phases, measured
+	 * slower, no longer fit two double-buffered workgroups per CU) */
 #define SPEC(LB, NT) hipLaunchKernelGGL((xa_decode_spec<BITS, CH, LB, NT>), \
     dim3(grid), dim3(per), 0, st, a)
 	const bool nt = (variant & 2u) != 0;
 	switch ((variant >> 2) & 3u) {
 	case 1:
 		if (nt) SPEC(128, true); else SPEC(128, false);
-		break;
-	case 2:
-		if (nt) SPEC(256, true); else SPEC(256, false);
 		break;
 	default:
 		if (nt) SPEC(64 * CH, true); else SPEC(64 * CH, false);
@@ -1039,7 +1094,7 @@ __global__ __launch_bounds__(64 * XA_SPEC_WPB) void
 xa_decode_spec_batch(xa_batch_args b)
 {
 	constexpr int R = batch_lds<LB>::REGION;
-	__shared__ __attribute__((aligned(16))) uint8_t lds[XA_SPEC_WPB * R];
+	__shared__ __attribute__((aligned(16))) uint8_t lds[XA_SPEC_WPB * 2 * R];
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const uint32_t w = blockIdx.x * XA_SPEC_WPB + wv;
 	if (w >= b.nwaves)
@@ -1049,9 +1104,9 @@ xa_decode_spec_batch(xa_batch_args b)
 	const uint32_t fmt = __builtin_amdgcn_readfirstlane(b.streams[sid].fmt);
 	const uint32_t wchunk0 = 64u * w -
 	    __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
-	uint8_t *region = lds + wv * R;
+	uint8_t *region = lds + wv * 2 * R;
 	with_format(fmt, [&](auto bc, auto cc) {
-		spec_wave<decltype(bc)::value, decltype(cc)::value, LB, NT>(a,
+		spec_wave<decltype(bc)::value, decltype(cc)::value, LB, NT, R>(a,
 		    region, wchunk0);
 	});
 }

@@ -1,0 +1,133 @@
+/*
+ * pattern_probe.hip -- read rate of the decode's input access pattern,
+ * isolated from the decode: every lane owns one "chunk" (a contiguous run of
+ * CB bytes) and walks it in steps of SEG bytes; a wave stages one step of its
+ * 64 lanes into LDS by 16-B LDS-DMA with the 64 segments concatenated (the
+ * K1 scheme), then every lane reads its segment back.  Variants:
+ *   SEG   bytes per lane per step (144 = K1's 8-bit group slot)
+ *   DEPTH steps in flight per wave (1: wait, consume, issue the next)
+ * plus a contiguous control (chunks interleaved so each DMA instruction reads
+ * 1 KiB of contiguous source).  Total bytes and waves match C3 (330 MB,
+ * 125,000 lanes).  Prints JSON lines.
+ *
+ * build: hipcc --offload-arch=gfx950 -O3 -o pattern_probe tools/pattern_probe.hip
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+	fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+__device__ __forceinline__ void
+dma16(const void *g, uint8_t *l)
+{
+	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 16, 0, 0);
+}
+
+template <int SEG, int DEPTH, bool CONTIG>
+__global__ __launch_bounds__(256) void
+k_pattern(const uint8_t *src, uint32_t *sink, uint32_t CB, uint32_t steps)
+{
+	constexpr int NP = SEG / 16;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * DEPTH * 64 * SEG];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *reg = lds + wv * DEPTH * 64 * SEG;
+	const uint64_t w = blockIdx.x * 4u + wv;
+	/* source byte of piece i of step s: strided chunks (lane t's segment at
+	 * chunk t, offset s*SEG) or contiguous (the wave's step s is one run
+	 * of 64*SEG bytes) */
+	uint32_t voff[NP];
+#pragma unroll
+	for (int i = 0; i < NP; i++) {
+		const int k = i * 64 + lane;
+		voff[i] = CONTIG ? (uint32_t)k * 16u :
+		    (uint32_t)(k / NP) * CB + (uint32_t)(k % NP) * 16u;
+	}
+	const uint8_t *wbase = src + w * 64ull * CB;
+	auto issue = [&](uint32_t s) {
+		const uint8_t *b = wbase + (CONTIG ? (uint64_t)s * 64 * SEG :
+		    (uint64_t)s * SEG);
+		uint8_t *l = reg + (s % DEPTH) * 64 * SEG;
+#pragma unroll
+		for (int i = 0; i < NP; i++)
+			dma16(b + voff[i], l + i * 64 * 16);
+	};
+	uint32_t acc = 0;
+#pragma unroll
+	for (int d = 0; d < DEPTH - 1; d++)
+		issue(d);
+	for (uint32_t s = 0; s < steps; s++) {
+		if (s + DEPTH - 1 < steps)
+			issue(s + DEPTH - 1);
+		if (DEPTH == 1)
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		else if (DEPTH == 2)
+			asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
+		else
+			asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NP) : "memory");
+		if (s + DEPTH - 1 >= steps)
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		const uint32_t *m = (const uint32_t *)(reg + (s % DEPTH) * 64 * SEG +
+		    lane * SEG);
+#pragma unroll
+		for (int i = 0; i < SEG / 4; i++)
+			acc += m[i];
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		__builtin_amdgcn_wave_barrier();
+	}
+	if (acc == 0x9e3779b9u)
+		*sink = acc;
+}
+
+template <int SEG, int DEPTH, bool CONTIG>
+static void
+run(const uint8_t *src, uint32_t *sink)
+{
+	/* 125,000 lanes (1,954 waves, 489 workgroups) as K1 on C3; chunk =
+	 * 40 eblocks x 66 B rounded to whole steps */
+	const uint32_t lanes = 125056, CB0 = 2640;
+	const uint32_t steps = CB0 / SEG, CB = steps * SEG;
+	const unsigned grid = lanes / 256;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL((k_pattern<SEG, DEPTH, CONTIG>), dim3(grid), dim3(256), 0, 0, src, sink, CB, steps);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL((k_pattern<SEG, DEPTH, CONTIG>), dim3(grid), dim3(256), 0, 0, src, sink, CB, steps);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)lanes * CB;
+	printf("{\"seg\": %d, \"depth\": %d, \"contig\": %d, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    SEG, DEPTH, CONTIG ? 1 : 0, ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
+int
+main()
+{
+	uint8_t *src;
+	uint32_t *sink;
+	CHECK(hipMalloc(&src, 400000000));
+	CHECK(hipMalloc(&sink, 4));
+	CHECK(hipMemset(src, 1, 400000000));
+	run<144, 1, false>(src, sink);
+	run<144, 2, false>(src, sink);
+	run<144, 3, false>(src, sink);
+	run<144, 1, true>(src, sink);
+	run<144, 2, true>(src, sink);
+	run<288, 1, false>(src, sink);
+	run<288, 2, false>(src, sink);
+	run<528, 1, false>(src, sink);
+	run<528, 1, true>(src, sink);
+	CHECK(hipDeviceSynchronize());
+	return 0;
+}
