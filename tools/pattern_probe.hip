@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <stdio.h>
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
 	fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
@@ -111,6 +112,129 @@ run(const uint8_t *src, uint32_t *sink)
 	hipEventDestroy(b);
 }
 
+
+/*
+ * K1 skeleton: the decode kernel's memory structure with a trivial "decode"
+ * (out dword i = in dword i % 33 ^ i): per step a lane consumes one 144-B
+ * input slot (132 B used) and emits 256 B (two 128-B lines).  Input: LDS-DMA
+ * into two alternating buffers (the next step's DMA issued before the work,
+ * counted vmcnt(16) wait).  Output: STAGE = lines staged in the consumed
+ * buffer and stored 8 whole lines per instruction (K1), or direct 16-B
+ * stores from VGPRs.  SIN/SOUT: lane-chunk strided (K1) or wave-contiguous.
+ */
+template <bool SIN, bool SOUT, bool STAGE>
+__global__ __launch_bounds__(256) void
+k_skel(const uint8_t *src, uint8_t *dst, uint32_t steps)
+{
+	constexpr int SEG = 144, NP = 9, LINE = 144, RS = 64 * SEG;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * RS];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *reg = lds + wv * 2 * RS;
+	const uint64_t w = blockIdx.x * 4u + wv;
+	const uint32_t CBI = steps * 132u, CBO = steps * 256u;
+	uint32_t voff[NP];
+#pragma unroll
+	for (int i = 0; i < NP; i++) {
+		const int k = i * 64 + lane;
+		voff[i] = SIN ? (uint32_t)(k / NP) * CBI + (uint32_t)(k % NP) * 16u :
+		    (uint32_t)k * 16u;
+	}
+	const uint8_t *wbi = src + w * 64ull * CBI;
+	uint8_t *wbo = dst + w * 64ull * CBO;
+	auto issue = [&](uint32_t s, uint8_t *l) {
+		const uint8_t *b = wbi + (SIN ? (uint64_t)s * 132u : (uint64_t)s * 64u * SEG);
+#pragma unroll
+		for (int i = 0; i < NP; i++)
+			dma16(b + voff[i], l + i * 64 * 16);
+	};
+	issue(0, reg);
+	int cur = 0;
+	for (uint32_t s = 0; s < steps; s++) {
+		uint8_t *cb = reg + (cur ? RS : 0), *ob = reg + (cur ? 0 : RS);
+		if (s != 0)
+			asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+		else
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		uint32_t win[33];
+		const uint32_t *m = (const uint32_t *)(cb + lane * SEG);
+#pragma unroll
+		for (int i = 0; i < 33; i++)
+			win[i] = m[i];
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		if (s + 1 < steps)
+			issue(s + 1, ob);
+		asm volatile("" ::: "memory");
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			u32x4 v[8];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const int i = h * 32 + q * 4 + j;
+					v[q][j] = win[i % 33] ^ (uint32_t)i;
+				}
+			/* this lane's 128-B line h of step s */
+			if (!STAGE) {
+				uint8_t *o = SOUT ? wbo + (uint64_t)lane * CBO + s * 256u + h * 128u :
+				    wbo + ((uint64_t)(s * 2 + h) * 64u + lane) * 128u;
+#pragma unroll
+				for (int q = 0; q < 8; q++)
+					__builtin_nontemporal_store(v[q], (u32x4 *)(o + q * 16));
+				continue;
+			}
+			uint8_t *line = cb + lane * LINE;
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				*(u32x4 *)(line + q * 16) = v[q];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			/* instruction i: lanes 8k..8k+7 store line 8i+k's pieces */
+#pragma unroll
+			for (int i = 0; i < 8; i++) {
+				const int ln = i * 8 + lane / 8, pc = lane % 8;
+				const u32x4 x = *(const u32x4 *)(cb + ln * LINE + pc * 16);
+				uint8_t *o = SOUT ? wbo + (uint64_t)ln * CBO + s * 256u + h * 128u + pc * 16u :
+				    wbo + ((uint64_t)(s * 2 + h) * 64u + ln) * 128u + pc * 16u;
+				__builtin_nontemporal_store(x, (u32x4 *)o);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		cur ^= 1;
+	}
+}
+
+template <bool SIN, bool SOUT, bool STAGE>
+static void
+run_skel(const uint8_t *src, uint8_t *dst)
+{
+	const uint32_t lanes = 125056, steps = 20;
+	const unsigned grid = lanes / 256;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL((k_skel<SIN, SOUT, STAGE>), dim3(grid), dim3(256), 0, 0, src, dst, steps);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL((k_skel<SIN, SOUT, STAGE>), dim3(grid), dim3(256), 0, 0, src, dst, steps);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)lanes * steps * (132 + 256);
+	printf("{\"skel\": 1, \"strided_in\": %d, \"strided_out\": %d, \"stage\": %d, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    SIN, SOUT, STAGE, ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
 int
 main()
 {
@@ -128,6 +252,14 @@ main()
 	run<288, 2, false>(src, sink);
 	run<528, 1, false>(src, sink);
 	run<528, 1, true>(src, sink);
+	uint8_t *dst;
+	CHECK(hipMalloc(&dst, 700000000));
+	run_skel<true, true, true>(src, dst);
+	run_skel<true, false, true>(src, dst);
+	run_skel<false, true, true>(src, dst);
+	run_skel<false, false, true>(src, dst);
+	run_skel<true, true, false>(src, dst);
+	run_skel<false, false, false>(src, dst);
 	CHECK(hipDeviceSynchronize());
 	return 0;
 }
