@@ -112,6 +112,33 @@ xa_step_lr(uint32_t t, xa_f2 k0, xa_f2 k1, xa_f2 &p0, xa_f2 &p1)
 	return fr;
 }
 
+/*
+ * One channel's step with the same f32 prediction (mono: one chain per
+ * lane, nothing to pack).  `th` is the int16 inflate value, shifted by
+ * range, in the low (HI = false) or high half of t:
+ *   v_pk_mul_f32/v_mul_f32 + v_fma_f32, v_cvt_i32_f32, v_add_u32_sdwa
+ *   (sext), v_med3_i32, v_cvt_f32_i32 -- 5 dependent operations, against
+ *   the integer step's 6 plus its separate range shift.
+ * Exactness as xa_step_lr; the clamp is explicit here.
+ */
+template <bool HI>
+__device__ __forceinline__ int32_t
+xa_step_f(uint32_t t, float k0, float k1, float &p0, float &p1)
+{
+#if defined(XA_DBG_STEP)
+	(void)k0;
+	(void)k1;
+	p1 = p0;
+	return (int32_t)(int16_t)(HI ? t >> 16 : t & 0xffffu);
+#endif
+	const float g = __builtin_fmaf(p0, k0, p1 * k1);
+	int32_t s = (int32_t)g + (int32_t)(int16_t)(HI ? t >> 16 : t & 0xffffu);
+	s = min(max(s, -32768), 32767);
+	p1 = p0;
+	p0 = (float)s;
+	return s;
+}
+
 /* per-channel K pair of a gain as the f32 factors of xa_step_lr */
 __device__ __forceinline__ void
 xa_gain_f(uint32_t gain, float &k0, float &k1)

@@ -57,6 +57,9 @@
 #ifndef XA_STEREO_LR
 #define XA_STEREO_LR 1		/* stereo K1 on the packed-f32 step */
 #endif
+#ifndef XA_MONO_F
+#define XA_MONO_F 1		/* mono K1 on the f32-prediction step */
+#endif
 
 /* ------------------------------------------------------------------ */
 
@@ -148,14 +151,14 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 	/* stereo: both chains in one packed-f32 instruction stream
 	 * (xa_step_lr); the int state converts in and out once per eblock */
 	xa_f2 f0 = {0.f, 0.f}, f1 = {0.f, 0.f}, fk0 = {0.f, 0.f}, fk1 = {0.f, 0.f};
-	uint32_t shp = 0;
-	if (CH == 2) {
-		f0 = xa_f2{(float)p0[0], (float)p0[CH - 1]};
-		f1 = xa_f2{(float)p1[0], (float)p1[CH - 1]};
-		fk0 = xa_f2{(float)k0[0], (float)k0[CH - 1]} * (1.0f / 256.0f);
-		fk1 = xa_f2{(float)k1[0], (float)k1[CH - 1]} * (1.0f / 256.0f);
-		shp = (sh[0] - 16u) | ((sh[CH - 1] - 16u) << 16);
-	}
+	uint32_t shp;
+	f0 = xa_f2{(float)p0[0], (float)p0[CH - 1]};
+	f1 = xa_f2{(float)p1[0], (float)p1[CH - 1]};
+	fk0 = xa_f2{(float)k0[0], (float)k0[CH - 1]} * (1.0f / 256.0f);
+	fk1 = xa_f2{(float)k1[0], (float)k1[CH - 1]} * (1.0f / 256.0f);
+	/* mono: both halves shift by the block's one range */
+	shp = (sh[0] - 16u) | ((sh[CH - 1] - 16u) << 16);
+	float m0 = f0.x, m1 = f1.x;	/* mono state */
 	/* 16-B piece q holds 4 stereo frames or 8 mono samples */
 #pragma unroll
 	for (int q = 0; q < 4 * CH; q++) {
@@ -186,6 +189,27 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 				    p1[CH - 1]);
 				fr[j] = __builtin_amdgcn_perm((uint32_t)sr,
 				    (uint32_t)sl, 0x05040100u);
+			} else if (XA_MONO_F) {
+				/* codes n, n+1 into the halves, one packed shift */
+				const int n = 8 * q + 2 * j;
+				uint32_t tp;
+				if (BITS == 8) {
+					const int b = O + 1 + n;
+					tp = __builtin_amdgcn_perm(w[(b + 1) >> 2],
+					    w[b >> 2], 0x000c000cu |
+					    (uint32_t)(b & 3) << 8 |
+					    (uint32_t)(((b + 1) >> 2) == (b >> 2) ?
+					    (b + 1) & 3 : 4 + ((b + 1) & 3)) << 24);
+				} else {
+					tp = __builtin_amdgcn_perm(
+					    (uint32_t)code_at<BITS>(w, O, n + 1),
+					    (uint32_t)code_at<BITS>(w, O, n), 0x07060302u);
+				}
+				const uint32_t t = xa_pk_ashr(tp, shp);
+				int32_t sa = xa_step_f<false>(t, fk0.x, fk1.x, m0, m1);
+				int32_t sb = xa_step_f<true>(t, fk0.x, fk1.x, m0, m1);
+				fr[j] = __builtin_amdgcn_perm((uint32_t)sb,
+				    (uint32_t)sa, 0x05040100u);
 			} else {
 				const int n = 8 * q + 2 * j;
 				int32_t sa = xa_step(code_at<BITS>(w, O, n), sh[0],
@@ -207,6 +231,10 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		/* keep the unpack of later codes from being hoisted here: it
 		 * would only raise register pressure */
 		__builtin_amdgcn_sched_barrier(0);
+	}
+	if (CH == 1 && XA_MONO_F) {
+		p0[0] = (int32_t)m0;
+		p1[0] = (int32_t)m1;
 	}
 	if (CH == 2 && XA_STEREO_LR) {
 		p0[0] = (int32_t)f0.x;
@@ -880,7 +908,7 @@ drain_tail(const xa_dec_args &a)
  * (only in workgroups that wrote) cheap.
  */
 #ifndef XA_FIX_CPT
-#define XA_FIX_CPT 4
+#define XA_FIX_CPT 2
 #endif
 
 template <int BITS, int CH>

@@ -122,12 +122,13 @@ run(const uint8_t *src, uint32_t *sink)
  * buffer and stored 8 whole lines per instruction (K1), or direct 16-B
  * stores from VGPRs.  SIN/SOUT: lane-chunk strided (K1) or wave-contiguous.
  */
-template <bool SIN, bool SOUT, bool STAGE>
+template <bool SIN, bool SOUT, bool STAGE, int PF = 0>
 __global__ __launch_bounds__(256) void
 k_skel(const uint8_t *src, uint8_t *dst, uint32_t steps)
 {
 	constexpr int SEG = 144, NP = 9, LINE = 144, RS = 64 * SEG;
 	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * RS];
+	__shared__ __attribute__((aligned(16))) uint8_t pfs[4 * 256];
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int lane = threadIdx.x & 63;
 	uint8_t *reg = lds + wv * 2 * RS;
@@ -152,10 +153,12 @@ k_skel(const uint8_t *src, uint8_t *dst, uint32_t steps)
 	int cur = 0;
 	for (uint32_t s = 0; s < steps; s++) {
 		uint8_t *cb = reg + (cur ? RS : 0), *ob = reg + (cur ? 0 : RS);
-		if (s != 0)
-			asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-		else
+		if (s == 0)
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		else if (PF && ((s - 1) % 4 == 0))
+			asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+		else
+			asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 		uint32_t win[33];
 		const uint32_t *m = (const uint32_t *)(cb + lane * SEG);
 #pragma unroll
@@ -164,6 +167,19 @@ k_skel(const uint8_t *src, uint8_t *dst, uint32_t steps)
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		if (s + 1 < steps)
 			issue(s + 1, ob);
+		if (PF && s % 4 == 0) {
+			/* pull this lane's input lines of steps s+PF .. s+PF+3 into
+			 * the caches in one burst (one dword per 128-B line) */
+			const uint8_t *b = src + (w * 64ull + lane) * CBI +
+			    (uint64_t)(s + PF) * 132u;
+			const uint8_t *lim = src + (w * 64ull + lane + 1) * CBI - 4;
+#pragma unroll
+			for (int k = 0; k < 5; k++) {
+				const uint8_t *a = b + k * 128;
+				__builtin_amdgcn_global_load_lds(a < lim ? a : lim,
+				    LDS_PTR(pfs + wv * 256), 4, 0, 0);
+			}
+		}
 		asm volatile("" ::: "memory");
 #pragma unroll
 		for (int h = 0; h < 2; h++) {
@@ -209,7 +225,7 @@ k_skel(const uint8_t *src, uint8_t *dst, uint32_t steps)
 	}
 }
 
-template <bool SIN, bool SOUT, bool STAGE>
+template <bool SIN, bool SOUT, bool STAGE, int PF = 0>
 static void
 run_skel(const uint8_t *src, uint8_t *dst)
 {
@@ -219,18 +235,18 @@ run_skel(const uint8_t *src, uint8_t *dst)
 	hipEventCreate(&a);
 	hipEventCreate(&b);
 	for (int i = 0; i < 2; i++)
-		hipLaunchKernelGGL((k_skel<SIN, SOUT, STAGE>), dim3(grid), dim3(256), 0, 0, src, dst, steps);
+		hipLaunchKernelGGL((k_skel<SIN, SOUT, STAGE, PF>), dim3(grid), dim3(256), 0, 0, src, dst, steps);
 	hipEventRecord(a, 0);
 	for (int i = 0; i < 20; i++)
-		hipLaunchKernelGGL((k_skel<SIN, SOUT, STAGE>), dim3(grid), dim3(256), 0, 0, src, dst, steps);
+		hipLaunchKernelGGL((k_skel<SIN, SOUT, STAGE, PF>), dim3(grid), dim3(256), 0, 0, src, dst, steps);
 	hipEventRecord(b, 0);
 	hipEventSynchronize(b);
 	float ms;
 	hipEventElapsedTime(&ms, a, b);
 	ms /= 20;
 	const double bytes = (double)lanes * steps * (132 + 256);
-	printf("{\"skel\": 1, \"strided_in\": %d, \"strided_out\": %d, \"stage\": %d, \"ms\": %.4f, \"TBs\": %.3f}\n",
-	    SIN, SOUT, STAGE, ms, bytes / ms / 1e9);
+	printf("{\"skel\": 1, \"strided_in\": %d, \"strided_out\": %d, \"stage\": %d, \"pf\": %d, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    SIN, SOUT, STAGE, PF, ms, bytes / ms / 1e9);
 	hipEventDestroy(a);
 	hipEventDestroy(b);
 }
@@ -258,8 +274,9 @@ main()
 	run_skel<true, false, true>(src, dst);
 	run_skel<false, true, true>(src, dst);
 	run_skel<false, false, true>(src, dst);
-	run_skel<true, true, false>(src, dst);
-	run_skel<false, false, false>(src, dst);
+	run_skel<true, true, true, 4>(src, dst);
+	run_skel<true, true, true, 8>(src, dst);
+	run_skel<true, true, true, 2>(src, dst);
 	CHECK(hipDeviceSynchronize());
 	return 0;
 }
