@@ -117,6 +117,92 @@ k_time(uint32_t seed, uint32_t neb, uint32_t *out)
 	out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
+
+/* dependent-chain latency: one wave per CU, every lane runs one chain of
+ * 32*nblk samples (codes from registers); cycles per sample from
+ * s_memtime around the loop.  V: 0 xa_step, 1 repair step (4-op chain),
+ * 2 xa_step_f, 3 xa_step_lr (per frame = two chains) */
+__device__ __forceinline__ int32_t
+lat_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0, int32_t &p1)
+{
+	const int32_t t256 = (top >> sh) << 8;
+	const int32_t c = __mul24(p1, k1) + t256;
+	const int32_t ha = __mul24(p0, k0) + c;
+	const int32_t hb = __mul24(p0, k0) + (c + 255);
+	const int32_t s = __builtin_amdgcn_fmed3f(0, 0, 0) == 0.f ?
+	    max(min(min(ha, 32767 * 256 + 255), max(hb, -32768 * 256)),
+	    min(max(min(ha, 32767 * 256 + 255), max(hb, -32768 * 256)), t256)) >> 8 : 0;
+	p1 = p0;
+	p0 = s;
+	return s;
+}
+
+template <int V>
+__global__ __launch_bounds__(64) void
+k_lat(uint32_t seed, uint32_t nblk, uint32_t *out, uint64_t *cyc)
+{
+	uint32_t s = seed ^ threadIdx.x * 2654435761u;
+	int32_t a0 = 0, a1 = 0;
+	float f0 = 0.f, f1 = 0.f;
+	xa_f2 q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
+	uint32_t acc = 0;
+	const uint64_t t0 = __builtin_amdgcn_s_memtime();
+	for (uint32_t e = 0; e < nblk; e++) {
+		const uint32_t prof = rnd(s);
+		const uint32_t g = (prof & 0xffu) % 5u, r = (prof >> 16) & 15u;
+		int32_t k0, k1;
+		xa_gain(g, k0, k1);
+		float fk0, fk1;
+		xa_gain_f(g, fk0, fk1);
+		uint32_t wl[8];
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			wl[i] = rnd(s);
+#pragma unroll
+		for (int n = 0; n < 32; n += 2) {
+			const uint32_t sel = 0x000c0c0cu | (uint32_t)(n & 3) << 24;
+			const int32_t ta = (int32_t)__builtin_amdgcn_perm(0u, wl[n >> 2], sel);
+			const int32_t tb = (int32_t)__builtin_amdgcn_perm(0u, wl[n >> 2], sel + (1u << 24));
+			if (V == 0) {
+				acc += xa_step(ta, 16u + r, k0, k1, a0, a1);
+				acc += xa_step(tb, 16u + r, k0, k1, a0, a1);
+			} else if (V == 1) {
+				acc += lat_step(ta, 16u + r, k0, k1, a0, a1);
+				acc += lat_step(tb, 16u + r, k0, k1, a0, a1);
+			} else if (V == 2) {
+				const uint32_t t = xa_pk_ashr(((uint32_t)ta >> 16) | ((uint32_t)tb & 0xffff0000u), r | r << 16);
+				acc += xa_step_f<false>(t, fk0, fk1, f0, f1);
+				acc += xa_step_f<true>(t, fk0, fk1, f0, f1);
+			} else {
+				const uint32_t t = xa_pk_ashr(((uint32_t)ta >> 16) | ((uint32_t)tb & 0xffff0000u), r | r << 16);
+				acc += xa_step_lr(t, xa_f2{fk0, fk0}, xa_f2{fk1, fk1}, q0, q1);
+			}
+		}
+	}
+	const uint64_t t1 = __builtin_amdgcn_s_memtime();
+	out[blockIdx.x * 64 + threadIdx.x] = acc;
+	if (threadIdx.x == 0)
+		cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int V>
+static double
+lat_run(uint32_t *o, uint64_t *c)
+{
+	const uint32_t nblk = 256;
+	hipLaunchKernelGGL((k_lat<V>), dim3(256), dim3(64), 0, 0, 3u, nblk, o, c);
+	hipLaunchKernelGGL((k_lat<V>), dim3(256), dim3(64), 0, 0, 3u, nblk, o, c);
+	hipDeviceSynchronize();
+	static uint64_t h[256];
+	hipMemcpy(h, c, sizeof h, hipMemcpyDeviceToHost);
+	double m = 0;
+	for (int i = 0; i < 256; i++)
+		m += (double)h[i];
+	m /= 256;
+	/* samples per lane: 32 per block (V 3: 16 frames = 32 samples) */
+	return m / (nblk * 32.0);
+}
+
 int
 main()
 {
@@ -162,5 +248,9 @@ main()
 	printf("{\"int_ms\": %.4f, \"lr_ms\": %.4f, \"lanes_differ\": %u, "
 	    "\"int_ns_per_frame_wave\": %.3f, \"lr_ns_per_frame_wave\": %.3f}\n",
 	    ms[0], ms[1], diff, ms[0] * 1e6 / (neb * 32) / 2, ms[1] * 1e6 / (neb * 32) / 2);
+	uint64_t *cy;
+	CHECK(hipMalloc(&cy, 256 * 8));
+	printf("{\"memtime_ticks_per_sample\": {\"int\": %.2f, \"repair\": %.2f, \"f32\": %.2f, \"lr_per_2\": %.2f}}\n",
+	    lat_run<0>(o1, cy), lat_run<1>(o1, cy), lat_run<2>(o1, cy), lat_run<3>(o1, cy));
 	return 0;
 }
