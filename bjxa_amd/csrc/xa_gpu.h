@@ -15,6 +15,9 @@ extern "C" {
 struct bjxa__gpu;
 
 /* NULL + errno (ENODEV without a GPU, ENOMEM) on failure */
+/* a HIP device is visible (checked once) */
+int bjxa__gpu_present(void);
+
 struct bjxa__gpu *bjxa__gpu_new(void);
 void bjxa__gpu_free(struct bjxa__gpu *g);
 

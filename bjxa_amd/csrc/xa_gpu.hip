@@ -29,8 +29,8 @@
 #define XA_VARIANT_STRUCT	0xfu	/* kernel structure, 0 = automatic */
 #define XA_VARIANT_BALANCED	0x20u	/* two-length chunk plan */
 
-static int
-gpu_present(void)
+extern "C" int
+bjxa__gpu_present(void)
 {
 	static int state;	/* 0 unknown, 1 yes, -1 no */
 	if (state == 0) {
@@ -143,7 +143,7 @@ bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream)
 		errno = EINVAL;
 		return -1;
 	}
-	if (!gpu_present()) {
+	if (!bjxa__gpu_present()) {
 		errno = ENODEV;
 		return -1;
 	}
@@ -171,7 +171,7 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 		errno = EINVAL;
 		return -1;
 	}
-	if (!gpu_present()) {
+	if (!bjxa__gpu_present()) {
 		errno = ENODEV;
 		return -1;
 	}
@@ -220,7 +220,7 @@ bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
 		errno = EINVAL;
 		return -1;
 	}
-	if (!gpu_present()) {
+	if (!bjxa__gpu_present()) {
 		errno = ENODEV;
 		return -1;
 	}
@@ -301,7 +301,7 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		}
 		cblocks += (uint64_t)s[i].eblocks * s[i].channels;
 	}
-	if (!gpu_present()) {
+	if (!bjxa__gpu_present()) {
 		errno = ENODEV;
 		return NULL;
 	}
@@ -479,7 +479,7 @@ grow(void **p, size_t *cap, size_t need)
 extern "C" struct bjxa__gpu *
 bjxa__gpu_new(void)
 {
-	if (!gpu_present()) {
+	if (!bjxa__gpu_present()) {
 		errno = ENODEV;
 		return NULL;
 	}
@@ -693,163 +693,3 @@ bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
 	return 0;
 }
 
-/* ------------------------------------------------------------------ */
-/* many host streams in one batched pass (bjxa_hip_decode_files)        */
-
-#ifdef XA_FILES_TIMING
-#include <stdio.h>
-#include <time.h>
-static double
-now_ms(void)
-{
-	struct timespec ts;
-	clock_gettime(CLOCK_MONOTONIC, &ts);
-	return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
-}
-#define TMARK(name) do { (void)hipStreamSynchronize(stream); \
-	fprintf(stderr, "%s %.2f\n", name, now_ms() - t0); } while (0)
-#else
-#define TMARK(name) do { } while (0)
-#endif
-
-extern "C" int
-bjxa__gpu_decode_many(struct bjxa__job *jobs, uint32_t n)
-{
-#ifdef XA_FILES_TIMING
-	const double t0 = now_ms();
-#endif
-	if (!gpu_present()) {
-		errno = ENODEV;
-		return -1;
-	}
-	size_t in_total = 0, out_total = 0;
-	for (uint32_t i = 0; i < n; i++) {
-		in_total += ((size_t)(jobs[i].bits * 4 + 1) * jobs[i].ch *
-		    jobs[i].eblocks + 15) & ~(size_t)15;
-		out_total += (size_t)jobs[i].eblocks * 64u * jobs[i].ch;
-	}
-	bjxa_hip_stream_t *hs = (bjxa_hip_stream_t *)calloc(n, sizeof *hs);
-	/* the callers' buffers are registered (pinned in place) for the call so
-	 * the copies are DMA straight from/to them; a range that cannot be
-	 * registered (e.g. shares a page with one that is) is copied as
-	 * pageable memory */
-	const char *reg_env = getenv("BJXA_FILES_REGISTER");
-	const bool reg = reg_env == NULL || strcmp(reg_env, "0") != 0;
-	uint8_t *regd = (uint8_t *)calloc(n, 2);
-	uint8_t *d_in = NULL, *d_out = NULL;
-	uint32_t *d_st = NULL, *st = (uint32_t *)malloc((size_t)n *
-	    BJXA_HIP_STATUS_WORDS * 4);
-	hipStream_t stream = NULL;
-	bjxa_hip_batch_t *b = NULL;
-	int rc = -1;
-
-	if (hs == NULL || st == NULL || regd == NULL) {
-		errno = ENOMEM;
-		goto out;
-	}
-	if (reg) {
-		for (uint32_t i = 0; i < n; i++) {
-			const size_t in_b = (size_t)(jobs[i].bits * 4 + 1) *
-			    jobs[i].ch * jobs[i].eblocks;
-			regd[2 * i] = in_b > 0 && hipHostRegister((void *)jobs[i].src,
-			    in_b, hipHostRegisterDefault) == hipSuccess;
-			regd[2 * i + 1] = jobs[i].dst_bytes > 0 &&
-			    hipHostRegister(jobs[i].dst, jobs[i].dst_bytes,
-			    hipHostRegisterDefault) == hipSuccess;
-		}
-		(void)hipGetLastError();	/* failed registrations are fine */
-	}
-	if (hipMalloc((void **)&d_in, in_total + 16) != hipSuccess ||
-	    hipMalloc((void **)&d_out, out_total + 16) != hipSuccess ||
-	    hipMalloc((void **)&d_st, (size_t)n * BJXA_HIP_STATUS_WORDS * 4) !=
-	    hipSuccess) {
-		errno = ENOMEM;
-		goto out;
-	}
-	if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) !=
-	    hipSuccess) {
-		stream = NULL;
-		errno = EIO;
-		goto out;
-	}
-	TMARK("alloc");
-	{
-		size_t oi = 0, oo = 0;
-		for (uint32_t i = 0; i < n; i++) {
-			const size_t in_b = (size_t)(jobs[i].bits * 4 + 1) *
-			    jobs[i].ch * jobs[i].eblocks;
-			if (hipMemcpyAsync(d_in + oi, jobs[i].src, in_b,
-			    hipMemcpyHostToDevice, stream) != hipSuccess) {
-				errno = EIO;
-				goto out;
-			}
-			hs[i].d_src = d_in + oi;
-			hs[i].d_dst = d_out + oo;
-			hs[i].eblocks = jobs[i].eblocks;
-			hs[i].frames = (uint64_t)jobs[i].eblocks * 32u;
-			hs[i].bits = jobs[i].bits;
-			hs[i].channels = jobs[i].ch;
-			memcpy(hs[i].state, jobs[i].state, sizeof hs[i].state);
-			oi += (in_b + 15) & ~(size_t)15;
-			oo += (size_t)jobs[i].eblocks * 64u * jobs[i].ch;
-		}
-	}
-	TMARK("h2d");
-	b = bjxa_hip_batch_new(hs, n, NULL, stream);
-	if (b == NULL)
-		goto out;
-	TMARK("plan");
-	if (bjxa_hip_batch_decode_async(b, d_st, NULL, stream) < 0)
-		goto out;
-	TMARK("decode");
-	if (hipMemcpyAsync(st, d_st, (size_t)n * BJXA_HIP_STATUS_WORDS * 4,
-	    hipMemcpyDeviceToHost, stream) != hipSuccess ||
-	    hipStreamSynchronize(stream) != hipSuccess) {
-		errno = EIO;
-		goto out;
-	}
-	for (uint32_t i = 0; i < n; i++) {
-		const uint32_t *w = st + (size_t)i * BJXA_HIP_STATUS_WORDS;
-		uint64_t bytes = jobs[i].dst_bytes;
-		jobs[i].err_cb = w[XA_ST_ERR];
-		if (w[XA_ST_ERR] != 0xffffffffu) {
-			const uint64_t cut = (uint64_t)(w[XA_ST_ERR] /
-			    jobs[i].ch) * 64u * jobs[i].ch;
-			if (bytes > cut)
-				bytes = cut;
-		}
-		if (bytes > 0 && hipMemcpyAsync(jobs[i].dst, hs[i].d_dst, bytes,
-		    hipMemcpyDeviceToHost, stream) != hipSuccess) {
-			errno = EIO;
-			goto out;
-		}
-	}
-	if (hipStreamSynchronize(stream) != hipSuccess) {
-		errno = EIO;
-		goto out;
-	}
-	TMARK("d2h");
-	rc = 0;
-out:
-	if (b != NULL)
-		bjxa_hip_batch_free(b);
-	TMARK("free_batch");
-	if (stream != NULL)
-		(void)hipStreamDestroy(stream);
-	(void)hipFree(d_in);
-	(void)hipFree(d_out);
-	(void)hipFree(d_st);
-	if (regd != NULL) {
-		for (uint32_t i = 0; i < n; i++) {
-			if (regd[2 * i])
-				(void)hipHostUnregister((void *)jobs[i].src);
-			if (regd[2 * i + 1])
-				(void)hipHostUnregister(jobs[i].dst);
-		}
-	}
-	free(regd);
-	free(hs);
-	free(st);
-	TMARK("free");
-	return rc;
-}

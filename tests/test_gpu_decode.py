@@ -158,3 +158,40 @@ def test_bef_entry_state(built, golden):
     hdr = bjxa_amd.xa_header(xa.size, 1000 * 32 - 5, 22050, 4, 2, st)
     wav = bjxa_amd.decode_file(hdr + xa.tobytes())
     assert wav == oracle.decode_file(hdr + xa.tobytes())
+
+
+_K = np.array([[0, 0], [240, 0], [460, -208], [392, -220], [488, -240]] +
+              [[0, 0]] * 11, dtype=np.int64)
+
+
+def _big_gain_steps(xa, eb, bits, ch, pcm):
+    """Predictor steps whose |p0*K0 + p1*K1| >= 2^24 (src/libbjxa.c:565),
+    where the kernels' f32 prediction rounds and only the int16 clamp makes
+    it exact."""
+    s = pcm.reshape(eb, 32, ch).astype(np.int64)
+    prof = xa.reshape(eb, ch, bits * 4 + 1)[:, :, 0].astype(np.int64)
+    n = 0
+    for c in range(ch):
+        x = s[:, :, c].reshape(-1)
+        g = (prof[:, c] >> 4).repeat(32)
+        p0 = np.concatenate([[0], x[:-1]])
+        p1 = np.concatenate([[0, 0], x[:-2]])
+        n += int(np.sum(np.abs(p0 * _K[g, 0] + p1 * _K[g, 1]) >= 1 << 24))
+    return n
+
+
+@pytest.mark.parametrize("ch", [1, 2])
+def test_f32_rounding_regime(built, ch):
+    """The f32 steps (xa_step_lr, xa_step_f) round p0*K0/256 + p1*K1/256 once
+    |g| >= 2^24; the stream must reach that regime often and still match
+    the oracle bit for bit."""
+    eb = 40000
+    xa = synth.stream(eb, 8, ch, "A", seed=1234 + ch).reshape(eb * ch, 33)
+    # every other channel block at gain 4, range 0 (uniform codes): the
+    # state swings across the whole int16 range, and about 1 % of the steps
+    # have |g| >= 2^24
+    xa[np.arange(eb * ch) % 2 == 0, 0] = 0x40
+    xa = xa.reshape(-1)
+    ref, _, _, _ = oracle.decode(xa, eb, 8, ch)
+    assert _big_gain_steps(xa, eb, 8, ch, ref) > 10000
+    assert np.array_equal(dev_decode(xa, eb, 8, ch), ref)

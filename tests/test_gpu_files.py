@@ -78,3 +78,38 @@ except bjxa_amd.BjxaError as e:
     lines = r.stdout.split("\n")
     assert lines[0] == str([errno.EPROTO, errno.ENOBUFS])
     assert lines[1] == str(errno.ENODEV)
+
+
+@pytest.mark.gpu
+def test_decode_files_multi_slab(built):
+    """A batch whose images span several 64 MiB staging slabs (input ~80 MB,
+    output ~160 MB): files of odd sizes straddle the slab cuts, the copy
+    pool splits pieces between threads, and a file that stops at a bad
+    profile in the middle of a slab keeps exactly its PCM prefix."""
+    rng = np.random.default_rng(11)
+    files = []
+    total = 0
+    i = 0
+    while total < 80_000_000:
+        bits, ch = [(8, 2), (6, 1), (4, 2), (8, 1)][i % 4]
+        eb = int(rng.integers(50_000, 400_000)) | 1
+        files.append(xa_file(eb, bits, ch, 900 + i, cut=int(rng.integers(0, 32))))
+        total += len(files[-1])
+        i += 1
+    k = len(files) // 2
+    bad = bytearray(files[k])
+    bits, ch = [(8, 2), (6, 1), (4, 2), (8, 1)][k % 4]
+    stop = 12345
+    bad[32 + stop * ch * (bits * 4 + 1)] = 0x60
+    files[k] = bytes(bad)
+    res = bjxa_amd.decode_files(files)
+    for j, (f, (wav, st)) in enumerate(zip(files, res)):
+        if j == k:
+            assert st == errno.EPROTO
+            full = oracle.decode(np.frombuffer(f, np.uint8, offset=32),
+                                 (len(f) - 32) // (ch * (bits * 4 + 1)), bits, ch)
+            assert full[2] == stop
+            assert wav[44:44 + stop * 64 * ch] == full[0][:stop * 32 * ch].tobytes()
+        else:
+            assert st == 0
+            assert wav == oracle.decode_file(f), j

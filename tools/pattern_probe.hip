@@ -251,6 +251,111 @@ run_skel(const uint8_t *src, uint8_t *dst)
 	hipEventDestroy(b);
 }
 
+/*
+ * K1 skeleton with one-eblock groups: a lane consumes 66 B (80-B slot) and
+ * emits 128 B per step as two 64-B lines, staged in the consumed buffer
+ * (64 x 80 B = 5 KiB per buffer, 10 KiB per wave: four 4-wave workgroups
+ * fit a CU).  Lanes/steps chosen by the caller at equal total bytes.
+ */
+__global__ __launch_bounds__(256) void
+k_skel1(const uint8_t *src, uint8_t *dst, uint32_t steps)
+{
+	constexpr int SEG = 80, NP = 5, LINE = 80, RS = 64 * SEG;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * 2 * RS];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *reg = lds + wv * 2 * RS;
+	const uint64_t w = blockIdx.x * 4u + wv;
+	const uint32_t CBI = steps * 66u, CBO = steps * 128u;
+	uint32_t voff[NP];
+#pragma unroll
+	for (int i = 0; i < NP; i++) {
+		const int k = i * 64 + lane;
+		voff[i] = (uint32_t)(k / NP) * CBI + (uint32_t)(k % NP) * 16u;
+	}
+	const uint8_t *wbi = src + w * 64ull * CBI;
+	uint8_t *wbo = dst + w * 64ull * CBO;
+	auto issue = [&](uint32_t s, uint8_t *l) {
+		const uint8_t *b = wbi + (uint64_t)s * 66u;
+#pragma unroll
+		for (int i = 0; i < NP; i++)
+			dma16(b + voff[i], l + i * 64 * 16);
+	};
+	issue(0, reg);
+	int cur = 0;
+	for (uint32_t s = 0; s < steps; s++) {
+		uint8_t *cb = reg + (cur ? RS : 0), *ob = reg + (cur ? 0 : RS);
+		if (s == 0)
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		else
+			asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+		uint32_t win[17];
+		const uint32_t *m = (const uint32_t *)(cb + lane * SEG);
+#pragma unroll
+		for (int i = 0; i < 17; i++)
+			win[i] = m[i];
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		if (s + 1 < steps)
+			issue(s + 1, ob);
+		asm volatile("" ::: "memory");
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			u32x4 v[4];
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const int i = h * 16 + q * 4 + j;
+					v[q][j] = win[i % 17] ^ (uint32_t)i;
+				}
+			uint8_t *line = cb + lane * LINE;
+#pragma unroll
+			for (int q = 0; q < 4; q++)
+				*(u32x4 *)(line + q * 16) = v[q];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			/* instruction i: lanes 4k..4k+3 store line 16i+k's pieces */
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				const int ln = i * 16 + lane / 4, pc = lane % 4;
+				const u32x4 x = *(const u32x4 *)(cb + ln * LINE + pc * 16);
+				uint8_t *o = wbo + (uint64_t)ln * CBO + s * 128u + h * 64u + pc * 16u;
+				__builtin_nontemporal_store(x, (u32x4 *)o);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		cur ^= 1;
+	}
+}
+
+static void
+run_skel1(const uint8_t *src, uint8_t *dst, uint32_t lanes, uint32_t steps)
+{
+	const unsigned grid = lanes / 256;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL(k_skel1, dim3(grid), dim3(256), 0, 0, src, dst, steps);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL(k_skel1, dim3(grid), dim3(256), 0, 0, src, dst, steps);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)grid * 256 * steps * (66 + 128);
+	printf("{\"skel1\": 1, \"lanes\": %u, \"steps\": %u, \"wgs\": %u, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    grid * 256, steps, grid, ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
 int
 main()
 {
@@ -274,9 +379,10 @@ main()
 	run_skel<true, false, true>(src, dst);
 	run_skel<false, true, true>(src, dst);
 	run_skel<false, false, true>(src, dst);
-	run_skel<true, true, true, 4>(src, dst);
-	run_skel<true, true, true, 8>(src, dst);
-	run_skel<true, true, true, 2>(src, dst);
+	run_skel1(src, dst, 125184, 40);
+	run_skel1(src, dst, 187392, 27);
+	run_skel1(src, dst, 250112, 20);
+	run_skel1(src, dst, 62720, 80);
 	CHECK(hipDeviceSynchronize());
 	return 0;
 }
