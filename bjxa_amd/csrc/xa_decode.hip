@@ -33,15 +33,20 @@
  *
  * Memory (K1).  Loops advance one "group" = 4 channel blocks (2 stereo or 4
  * mono eblocks) = 4*(bits*4+1) bytes, a whole number of dwords.  Each wave
- * owns two LDS regions:
+ * owns two LDS buffers and alternates them group by group:
  *  - input: the group of each of its 64 chunks, fetched by LDS-DMA with the
- *    64 segments concatenated so every DMA instruction reads 64 x 4/12/16
- *    contiguous bytes (instead of 64 scattered 16-B pieces, which saturated
- *    the texture addresser).  A lane copies its segment to VGPRs and the next group's
- *    DMA is issued at once, overlapping the decode.
- *  - output: one 64-B line per lane (a mono block, or half a stereo eblock),
- *    written back so each store instruction covers 16 whole 64-B lines.
- *    The DMA wait is a counted vmcnt that leaves those stores in flight.
+ *    64 segments concatenated, so every DMA instruction fills 1 KiB of LDS
+ *    from a few 144-B runs of the stream (instead of 64 scattered 16-B
+ *    pieces, which saturated the texture addresser).  A lane copies its
+ *    segment to VGPRs and the next group's DMA is issued into the other
+ *    buffer at once, so it lands while this group decodes.
+ *  - output: the group's PCM is staged 128 B per lane in the buffer just
+ *    consumed and stored so that each instruction covers 8 whole lines.
+ *    The wait for the next group's DMA is vmcnt(16): it leaves this
+ *    group's 16 stores in flight.
+ * Predictor: stereo runs both channels as the two halves of packed-f32
+ * instructions (xa_step_lr), mono a single f32 chain (xa_step_f); both are
+ * exact (xa_common.h).
  */
 #include <type_traits>
 
@@ -53,12 +58,6 @@
 #endif
 #ifndef XA_DMA_AUX
 #define XA_DMA_AUX 0		/* cache policy bits of the input LDS-DMA */
-#endif
-#ifndef XA_STEREO_LR
-#define XA_STEREO_LR 1		/* stereo K1 on the packed-f32 step */
-#endif
-#ifndef XA_MONO_F
-#define XA_MONO_F 1		/* mono K1 on the f32-prediction step */
 #endif
 
 /* ------------------------------------------------------------------ */
@@ -148,16 +147,16 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		xa_gain(gain & 7u, k0[c], k1[c]);
 		bad |= (gain >= 5u) ? (1u << c) : 0u;
 	}
-	/* stereo: both chains in one packed-f32 instruction stream
-	 * (xa_step_lr); the int state converts in and out once per eblock */
-	xa_f2 f0 = {0.f, 0.f}, f1 = {0.f, 0.f}, fk0 = {0.f, 0.f}, fk1 = {0.f, 0.f};
-	uint32_t shp;
-	f0 = xa_f2{(float)p0[0], (float)p0[CH - 1]};
-	f1 = xa_f2{(float)p1[0], (float)p1[CH - 1]};
-	fk0 = xa_f2{(float)k0[0], (float)k0[CH - 1]} * (1.0f / 256.0f);
-	fk1 = xa_f2{(float)k1[0], (float)k1[CH - 1]} * (1.0f / 256.0f);
-	/* mono: both halves shift by the block's one range */
-	shp = (sh[0] - 16u) | ((sh[CH - 1] - 16u) << 16);
+	/* f32 state for the block (xa_common.h): stereo runs both chains in
+	 * one packed instruction stream (xa_step_lr), mono one chain
+	 * (xa_step_f); the int state converts in and out once per eblock.
+	 * shp: the range of each half of a packed code pair (mono: both
+	 * halves are the block's one range) */
+	xa_f2 f0 = {(float)p0[0], (float)p0[CH - 1]};
+	xa_f2 f1 = {(float)p1[0], (float)p1[CH - 1]};
+	const xa_f2 fk0 = xa_f2{(float)k0[0], (float)k0[CH - 1]} * (1.0f / 256.0f);
+	const xa_f2 fk1 = xa_f2{(float)k1[0], (float)k1[CH - 1]} * (1.0f / 256.0f);
+	const uint32_t shp = (sh[0] - 16u) | ((sh[CH - 1] - 16u) << 16);
 	float m0 = f0.x, m1 = f1.x;	/* mono state */
 	/* 16-B piece q holds 4 stereo frames or 8 mono samples */
 #pragma unroll
@@ -165,7 +164,7 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		uint32_t fr[4];
 #pragma unroll
 		for (int j = 0; j < 4; j++) {
-			if (CH == 2 && XA_STEREO_LR) {
+			if (CH == 2) {
 				const int n = 4 * q + j;
 				uint32_t tp;
 				if (BITS == 8) {
@@ -180,16 +179,7 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 					    (uint32_t)code_at<BITS>(w, O, n), 0x07060302u);
 				}
 				fr[j] = xa_step_lr(xa_pk_ashr(tp, shp), fk0, fk1, f0, f1);
-			} else if (CH == 2) {
-				const int n = 4 * q + j;
-				int32_t sl = xa_step(code_at<BITS>(w, O, n), sh[0],
-				    k0[0], k1[0], p0[0], p1[0]);
-				int32_t sr = xa_step(code_at<BITS>(w, O + BSZ, n),
-				    sh[CH - 1], k0[CH - 1], k1[CH - 1], p0[CH - 1],
-				    p1[CH - 1]);
-				fr[j] = __builtin_amdgcn_perm((uint32_t)sr,
-				    (uint32_t)sl, 0x05040100u);
-			} else if (XA_MONO_F) {
+			} else {
 				/* codes n, n+1 into the halves, one packed shift */
 				const int n = 8 * q + 2 * j;
 				uint32_t tp;
@@ -210,14 +200,6 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 				int32_t sb = xa_step_f<true>(t, fk0.x, fk1.x, m0, m1);
 				fr[j] = __builtin_amdgcn_perm((uint32_t)sb,
 				    (uint32_t)sa, 0x05040100u);
-			} else {
-				const int n = 8 * q + 2 * j;
-				int32_t sa = xa_step(code_at<BITS>(w, O, n), sh[0],
-				    k0[0], k1[0], p0[0], p1[0]);
-				int32_t sb = xa_step(code_at<BITS>(w, O, n + 1), sh[0],
-				    k0[0], k1[0], p0[0], p1[0]);
-				fr[j] = __builtin_amdgcn_perm((uint32_t)sb,
-				    (uint32_t)sa, 0x05040100u);
 			}
 		}
 		if (STORE) {
@@ -232,11 +214,11 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 		 * would only raise register pressure */
 		__builtin_amdgcn_sched_barrier(0);
 	}
-	if (CH == 1 && XA_MONO_F) {
+	if (CH == 1) {
 		p0[0] = (int32_t)m0;
 		p1[0] = (int32_t)m1;
 	}
-	if (CH == 2 && XA_STEREO_LR) {
+	if (CH == 2) {
 		p0[0] = (int32_t)f0.x;
 		p0[CH - 1] = (int32_t)f0.y;
 		p1[0] = (int32_t)f1.x;
