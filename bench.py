@@ -416,7 +416,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32",
+        "dtype": "int32+f32",
         "data": "synthetic (seeded XA stream, profile mix %s, uniform codes)" % args.mix,
         "config": {"workload": r["desc"] + " per rank", "workload_id": args.workload,
                    "bits": r["bits"], "channels": r["ch"],
@@ -458,7 +458,7 @@ def main_c5(args, dev, world, rank):
         "value": round(total * args.steps / elapsed / 1e6, 1), "unit": "MSamples/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+        "scaling": "strong", "vs_baseline": None, "dtype": "int32+f32",
         "data": "synthetic (seeded XA streams, profile mix A, uniform codes)",
         "config": {"workload": BATCHES["C5"], "workload_id": "C5",
                    "streams_per_rank": r["streams"],
