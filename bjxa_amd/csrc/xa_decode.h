@@ -25,6 +25,13 @@
 #define XA_ST_W		7
 #define XA_ST_WORDS	8
 
+/*
+ * Chunk and warm-up lengths are whole multiples of this many eblocks (8
+ * channel blocks): K1 moves a lane's input two groups of 4 channel blocks
+ * at a time.
+ */
+#define XA_CHUNK_Q(ch)	(8u / (ch))
+
 struct xa_dec_args {
 	const uint8_t *src;	/* XA blocks, eblock b at src + b*ch*(bits*4+1) */
 	uint8_t *dst;		/* PCM, eblock b at dst + b*64*ch */
@@ -32,9 +39,9 @@ struct xa_dec_args {
 	uint32_t eblocks;
 	uint32_t nchunks;
 	uint32_t C, W;		/* chunk and warm-up lengths in eblocks */
-	uint32_t nlong;		/* chunks [0, nlong) are C + G long (G = 4 / ch,
-				 * nlong % 64 == 0); chunk q starts at eblock
-				 * q*C + G*min(q, nlong) */
+	uint32_t nlong;		/* chunks [0, nlong) are C + Q long (Q =
+				 * XA_CHUNK_Q(ch), nlong % 64 == 0); chunk q
+				 * starts at eblock q*C + Q*min(q, nlong) */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
 	uint2 *g, *e;		/* per-chunk entry / exit state */
 	uint32_t *queue;	/* re-check queue, nchunks entries */

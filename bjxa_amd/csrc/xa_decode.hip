@@ -95,23 +95,12 @@ template <int BITS, int CH> struct geo {
 	static constexpr int BSZ = BITS * 4 + 1;	/* channel block */
 	static constexpr int EBSZ = BSZ * CH;		/* effective block */
 	static constexpr int G = 4 / CH;		/* eblocks per group */
+	static constexpr int G2 = XA_CHUNK_Q(CH);	/* chunk granularity */
 	static constexpr int GDW = BSZ;			/* dwords per group */
 	static constexpr int OB = 64 * CH;		/* PCM bytes per eblock */
-	/* LDS-DMA: 16-B pieces (packed lane-linear in LDS at any 4-B aligned
-	 * source; 12-B pieces are not: they land at a 16-B lane stride), so a
-	 * group's segment is read rounded up to SEGB bytes -- the extra bytes
-	 * are the start of the chunk's next group -- and segments sit SEGB
-	 * apart in LDS (8-bit: 144 B = 36 dwords, 16 lanes of a ds_read_b128
-	 * phase hit all 64 banks once) */
-#ifndef XA_DMA_MAXPIECE
-#define XA_DMA_MAXPIECE 16
-#endif
-	static constexpr int PS = XA_DMA_MAXPIECE >= 16 ? 16 : 4;
-	static constexpr int SEGB = (GDW * 4 + PS - 1) / PS * PS;
-	static constexpr int NP = SEGB / PS;		/* pieces per segment */
 };
 
-/* first eblock of chunk q (chunks [0, nlong) are G longer) */
+/* first eblock of chunk q (chunks [0, nlong) are G longer; G = G2) */
 template <int G>
 __device__ __forceinline__ int64_t
 chunk_start(const xa_dec_args &a, uint32_t q)
@@ -333,62 +322,9 @@ dma<4>(const void *g, uint8_t *l)
 	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 4, 0, XA_DMA_AUX);
 }
 template <> __device__ __forceinline__ void
-dma<12>(const void *g, uint8_t *l)
-{
-	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 12, 0, XA_DMA_AUX);
-}
-template <> __device__ __forceinline__ void
 dma<16>(const void *g, uint8_t *l)
 {
 	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 16, 0, XA_DMA_AUX);
-}
-
-/*
- * Stage one group of each of the wave's 64 chunks into `ibuf` by LDS-DMA:
- * the 64 segments (SEGB bytes each) are concatenated and cut into PS-byte
- * pieces; instruction i moves pieces [64i, 64i+64) of that concatenation
- * (lane t: piece 64i+t), i.e. 64*PS contiguous bytes of one or two
- * segments.  The wave's chunks start at eblock wstart and are Cw long.
- * `rel` is the group's first eblock relative to each chunk's start.
- * Segments outside the stream (warm-up before eblock 0, the ragged end) are
- * clamped onto valid bytes; their lanes never decode them.
- */
-template <int BITS, int CH>
-__device__ __forceinline__ void
-stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, int64_t wstart,
-    uint32_t Cw, int64_t rel, const uint32_t *voff)
-{
-	typedef geo<BITS, CH> g;
-	constexpr int NP = g::NP, PS = g::PS;
-	const int64_t e_first = wstart + rel;
-	const int64_t e_end = wstart + 63 * (int64_t)Cw + rel + g::G;
-	/* the last segment's read may run SEGB - 4*GDW bytes past its group */
-	if (e_first >= 0 && e_end * g::EBSZ + (g::SEGB - 4 * g::GDW) <=
-	    (int64_t)a.eblocks * g::EBSZ) {
-		const uint8_t *base = a.src + (size_t)e_first * g::EBSZ;
-#pragma unroll
-		for (int i = 0; i < NP; i++)
-			dma<PS>(base + voff[i], ibuf + i * 64 * PS);
-		return;
-	}
-	/* rare path (the grid's first and last waves): dword pieces into the
-	 * same SEGB-strided layout, each clamped into the stream whole (the
-	 * dword holding the stream's last byte is read whole, nothing past
-	 * it).  Launder the inputs so none of its arithmetic is hoisted into
-	 * the caller's loops. */
-	uint32_t C = Cw, neb = a.eblocks;
-	int64_t r = wstart + rel;
-	const uint8_t *src = a.src;
-	asm volatile("" : "+v"(C), "+v"(neb), "+v"(r), "+v"(src));
-	constexpr int SD = g::SEGB / 4;
-	const int64_t last = ((int64_t)neb * g::EBSZ - 1) & ~(int64_t)3;
-#pragma nounroll
-	for (int i = 0; i < SD; i++) {
-		const int k = i * 64 + lane, seg = k / SD, off = k % SD;
-		int64_t byte = ((int64_t)seg * C + r) * g::EBSZ + off * 4;
-		byte = byte < 0 ? 0 : (byte > last ? last : byte);
-		dma<4>(src + byte, ibuf + i * 256);
-	}
 }
 
 /*
@@ -401,54 +337,112 @@ stage_group(const xa_dec_args &a, uint8_t *ibuf, int lane, int64_t wstart,
  * next group's DMA is issued.  (Separate regions with the DMA issued before
  * the decode and a counted vmcnt measured no faster)
  */
-/* per-wave LDS region of K1 */
-template <int BITS, int CH, int LB> struct spec_lds {
-	static constexpr int IBUF = 64 * geo<BITS, CH>::SEGB;	/* input */
-	static constexpr int LINE = LB + 16;		/* output line + pad */
-	static constexpr int OBUF = 64 * LINE;		/* output stage */
-	static constexpr int REGION = IBUF > OBUF ? IBUF : OBUF;
-};
 
 /*
  * K1 body: one wave decodes chunks wchunk0 .. wchunk0+63 of stream `a`
- * (wave-uniform), staging through the wave's two LDS buffers `region` and
- * `region + RS`.  In the chunk phase they alternate: group s is copied out
- * of buffer s&1 into VGPRs, group s+1's DMA is issued into the other buffer
- * at once, and group s's output lines are staged in buffer s&1 (free after
- * the copy).  So the DMA lands while the group decodes, and the wait for it
- * (vmcnt(XA_NST): all but the group's own 16 stores, which count in issue
- * order) leaves the stores in flight.
+ * (wave-uniform) with two-group input runs.  A lane's input for a
+ * "super-step" (two groups, 2G eblocks) is one contiguous run of 8*GDW
+ * bytes.  The runs of half a wave (32 lanes) land together in one LDS
+ * buffer, so a DMA instruction reads two runs of ~264 B instead of seven
+ * 144-B segments (fewer, longer DRAM bursts: the K1 skeleton of
+ * tools/pattern_probe.hip runs 4.5 % faster this way), and each lane keeps
+ * its run in VGPRs.  The next super-step's two halves land while this one
+ * decodes: half 0 before the first group, half 1 before the second, each
+ * wait leaving the previous group's 16 stores in flight.  Output lines are
+ * staged in a separate region as before.
  */
 #define XA_NST 16	/* store instructions per group (G * OB / 16) */
-template <int BITS, int CH, int LB, bool NT, int RS>
+
+template <int BITS, int CH> struct geo2 {
+	typedef geo<BITS, CH> g;
+	static constexpr int RD = 2 * g::GDW;			/* dwords per run */
+	static constexpr int SLOT = (RD * 4 + 15) / 16 * 16;	/* LDS bytes per run */
+	static constexpr int NPR = SLOT / 16;			/* 16-B pieces per run */
+	static constexpr int NI = (32 * NPR + 63) / 64;		/* DMA instructions per half */
+	static constexpr int LAST = 32 * NPR - 64 * (NI - 1);	/* lanes of the last one */
+	static constexpr int HALF = 32 * SLOT;
+};
+
+template <int BITS, int CH, int LB> struct spec_lds2 {
+	static constexpr int LINE = LB + 16;
+	static constexpr int REGION = geo2<BITS, CH>::HALF + 64 * LINE;
+};
+
+/*
+ * Stage the runs of half h of the wave (chunks 32h .. 32h+31 of the wave)
+ * that start `rel` eblocks into their chunks.  Piece k of the landing image
+ * is run k / NPR, bytes 16 (k % NPR) ... (voff).  Runs that reach outside
+ * the stream (the grid's first and last waves) take dword pieces, each
+ * clamped into the stream whole (the dword holding the stream's last byte
+ * is read whole, nothing past it); their lanes never decode those bytes.
+ * LDS-DMA facts (tools/dma_probe.hip): 16-B pieces land packed lane-linear
+ * in LDS even from 4-B aligned sources; 12-B pieces land at a 16-B lane
+ * stride, so runs are read rounded up to 16 B (SLOT).
+ */
+template <int BITS, int CH>
 __device__ __forceinline__ void
-spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
+stage_half(const xa_dec_args &a, uint8_t *land, int lane, int64_t wstart,
+    uint32_t Cw, int h, int64_t rel, const uint32_t *voff)
 {
 	typedef geo<BITS, CH> g;
-	typedef spec_lds<BITS, CH, LB> L;
+	typedef geo2<BITS, CH> g2;
+	const int64_t c0 = wstart + (int64_t)h * 32 * Cw;
+	const int64_t e_first = c0 + rel;
+	const int64_t e_end = c0 + 31 * (int64_t)Cw + rel + 2 * g::G;
+	if (e_first >= 0 && e_end * g::EBSZ + (g2::SLOT - 4 * g2::RD) <=
+	    (int64_t)a.eblocks * g::EBSZ) {
+		const uint8_t *base = a.src + (size_t)e_first * g::EBSZ;
+#pragma unroll
+		for (int i = 0; i < g2::NI; i++)
+			if (i < g2::NI - 1 || lane < g2::LAST)
+				dma<16>(base + voff[i], land + i * 1024);
+		return;
+	}
+	uint32_t C = Cw, neb = a.eblocks;
+	int64_t r = c0 + rel;
+	const uint8_t *src = a.src;
+	asm volatile("" : "+v"(C), "+v"(neb), "+v"(r), "+v"(src));
+	constexpr int SD = g2::SLOT / 4;
+	const int64_t last = ((int64_t)neb * g::EBSZ - 1) & ~(int64_t)3;
+#pragma nounroll
+	for (int i = 0; i < (32 * SD + 63) / 64; i++) {
+		const int k = i * 64 + lane, run = k / SD, off = k % SD;
+		if (k >= 32 * SD)
+			continue;
+		int64_t byte = ((int64_t)run * C + r) * g::EBSZ + off * 4;
+		byte = byte < 0 ? 0 : (byte > last ? last : byte);
+		dma<4>(src + byte, land + i * 256);
+	}
+}
+
+template <int BITS, int CH, int LB, bool NT>
+__device__ __forceinline__ void
+spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
+{
+	typedef geo<BITS, CH> g;
+	typedef geo2<BITS, CH> g2;
 	constexpr int G = g::G, OB = g::OB, EBSZ = g::EBSZ, GDW = g::GDW;
-	constexpr int LINE = L::LINE;
+	constexpr int RD = g2::RD, LINE = LB + 16;
+	static_assert(G * OB / 16 == XA_NST, "store count per group");
 
 	const int lane = threadIdx.x & 63;
-	static_assert(G * OB / 16 == XA_NST, "store count per group");
-	static_assert(RS >= L::REGION, "buffer stride");
-	uint8_t *ibuf = region;
+	uint8_t *land = region, *ost = region + g2::HALF;
 	const uint32_t chunk = wchunk0 + lane;
 	const int64_t eblocks = a.eblocks;
-	/* the wave's chunks are all long or all short (nlong % 64 == 0) */
-	const uint32_t Cw = a.C + (wchunk0 < a.nlong ? (uint32_t)G : 0u);
-	const int64_t wstart = chunk_start<G>(a, wchunk0);
+	const uint32_t Cw = a.C + (wchunk0 < a.nlong ? (uint32_t)g::G2 : 0u);
+	const int64_t wstart = chunk_start<g::G2>(a, wchunk0);
 	const int64_t b0 = wstart + (int64_t)lane * Cw;
 	const int W = (int)a.W;
+	/* super-steps: NW of warm-up, then NC of the chunk (W and Cw are
+	 * multiples of 2G, the host plans them so) */
+	const int NW = W / (2 * G), NS = NW + (int)Cw / (2 * G);
 
-	/* DMA source offsets (bytes from the wave's segment 0) of this lane's
-	 * piece in each stage instruction; the same for every group */
-	constexpr int NP = g::NP, PS = g::PS;
-	uint32_t voff[NP];
+	uint32_t voff[g2::NI];
 #pragma unroll
-	for (int i = 0; i < NP; i++) {
+	for (int i = 0; i < g2::NI; i++) {
 		const int k = i * 64 + lane;
-		voff[i] = (uint32_t)(k / NP) * Cw * EBSZ + (uint32_t)(k % NP) * PS;
+		voff[i] = (uint32_t)(k / g2::NPR) * Cw * EBSZ +
+		    (uint32_t)(k % g2::NPR) * 16u;
 	}
 
 	int32_t p0[CH], p1[CH];
@@ -459,81 +453,69 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 		else
 			p0[c] = p1[c] = 0;
 	}
+	uint32_t gst[2] = { 0u, 0u };
 
-	uint32_t w[GDW];
-	const uint32_t *mine = (const uint32_t *)(ibuf + lane * g::SEGB);
-	uint8_t *line = ibuf + lane * LINE;
-	auto none = [](int) {};
-	stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, -W, voff);
-
-	/* warm-up: state only; the next group's DMA overlaps the decode */
-	for (int rel = -W; rel < 0; rel += G) {
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-		for (int i = 0; i < GDW; i++)
-			w[i] = mine[i];
-		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-		stage_group<BITS, CH>(a, ibuf, lane, wstart, Cw, rel + G, voff);
-		auto body = [&](auto uc) {
-			constexpr int u = decltype(uc)::value;
-			const int64_t b = b0 + rel + u;
-			if (b >= 0 && b < eblocks)
-				(void)decode_eblock<BITS, CH, false, true, 64>(w,
-				    u * EBSZ, p0, p1, line, none);
-		};
-		sfor<0, G>::run(body);
-	}
-	uint32_t gst[2];
-	gst[0] = xa_pack_state(p0[0], p1[0]);
-	gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
-
-	/* the chunk: decode, stage 64-B lines, write them back whole */
 	const uint32_t chunk_bytes = Cw * OB;
 	const uint64_t wstart_b = (uint64_t)wstart * OB;
 	constexpr int P = LB / 16;
 	uint8_t *gbase = a.dst + wstart_b + (uint64_t)(lane / P) * chunk_bytes +
 	    (lane % P) * 16;
-	const uint32_t lofs = (lane / P) * LINE + (lane % P) * 16;
-	/* every line of this wave lies before the stream's first cut block */
+	const uint8_t *lbase = ost + (lane / P) * LINE + (lane % P) * 16;
+	uint8_t *line = ost + lane * LINE;
 	const uint64_t full_blocks = a.pcm_bytes / OB;
 	const bool wave_full = wchunk0 + 63u < a.nchunks &&
 	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
 	const bool clean = (a.pcm_bytes & 15u) == 0;
-	int cur = 0;	/* buffer holding the group about to be decoded */
-	for (int s0 = 0; s0 < (int)Cw; s0 += G) {
-		uint8_t *cb = region + (cur ? RS : 0), *ob = region + (cur ? 0 : RS);
+	auto none = [](int) {};
+
+	/* copy this lane's run out of the landing buffer (half h only) */
+	auto take = [&](int h, uint32_t *dst) {
+		if ((lane >> 5) == h) {
+			const uint32_t *m = (const uint32_t *)(land +
+			    (lane & 31) * g2::SLOT);
+#pragma unroll
+			for (int i = 0; i < RD; i++)
+				dst[i] = m[i];
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	};
+	auto rel_of = [&](int S) -> int64_t { return (int64_t)S * 2 * G - W; };
+	/* wait for the DMA issued just before decoding group gi: only that
+	 * group's stores are younger, when it stored on the fast path */
+	auto wait_after = [&](int gi) {
 #ifndef XA_DBG_NOSTORE
-		/* the group's DMA is older than the previous group's XA_NST
-		 * stores (fast path only; the edge paths store per piece) */
-		if (s0 != 0 && wave_full)
+		if (gi >= 2 * NW && wave_full)
 			asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA_NST) : "memory");
 		else
 #endif
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		mine = (const uint32_t *)(cb + lane * g::SEGB);
-		line = cb + lane * LINE;
-		const uint8_t *obuf = cb, *lbase = cb + lofs;
-#pragma unroll
-		for (int i = 0; i < GDW; i++)
-			w[i] = mine[i];
-		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-		if (s0 + G < (int)Cw)
-			stage_group<BITS, CH>(a, ob, lane, wstart, Cw, s0 + G, voff);
-		asm volatile("" ::: "memory");
+	};
+
+	/* decode group hh (0/1) of super-step S from run r */
+	auto group = [&](const uint32_t *r, int S, auto hc) {
+		constexpr int hh = decltype(hc)::value;
+		if (S < NW) {
+			auto body = [&](auto uc) {
+				constexpr int u = decltype(uc)::value;
+				const int64_t b = b0 + rel_of(S) + hh * G + u;
+				if (b >= 0 && b < eblocks)
+					(void)decode_eblock<BITS, CH, false, true, 64>(r,
+					    hh * 4 * GDW + u * EBSZ, p0, p1, line, none);
+			};
+			sfor<0, G>::run(body);
+			return;
+		}
+		const int s0 = (S - NW) * 2 * G + hh * G;
 		auto body = [&](auto uc) {
 			constexpr int u = decltype(uc)::value;
-			const int s = s0 + u;
-			const int64_t b = b0 + s;
+			const int64_t b = b0 + s0 + u;
 			auto flush = [&](int h) {
 				wave_lds_sync();
-				store_lines<LB, NT>(a, obuf, lane, wchunk0, wstart_b,
+				store_lines<LB, NT>(a, ost, lane, wchunk0, wstart_b,
 				    chunk_bytes, (uint32_t)s0 * OB + (uint32_t)LB * h,
 				    wave_full, clean, gbase, lbase);
 				wave_lds_sync();
 			};
-			/* every lane runs the decode (flush holds wave-wide
-			 * stores); past the stream's end -- only in the last
-			 * chunk -- it decodes padding and keeps its old state */
 			const bool act = b < eblocks;
 			int32_t q0[CH], q1[CH];
 #pragma unroll
@@ -542,7 +524,8 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 				q1[c] = p1[c];
 			}
 			uint32_t bad = decode_eblock<BITS, CH, true, true, LB,
-			    u * 4 * CH>(w, u * EBSZ, p0, p1, line, flush);
+			    u * 4 * CH>(r, hh * 4 * GDW + u * EBSZ, p0, p1, line,
+			    flush);
 			if (act && bad) {
 				uint32_t cb = (uint32_t)b * CH + ((bad & 1u) ? 0u : 1u);
 				atomicMin(&a.ctl[XA_CTL_ERR], cb);
@@ -554,9 +537,59 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 			}
 		};
 		sfor<0, G>::run(body);
-		/* the staged lines have been read back (the stores hold VGPRs) */
+	};
+
+	/* one super-step from run `cur`, landing the next one into `nxt` */
+	auto step = [&](int S, uint32_t *cur, uint32_t *nxt) {
+		if (S == NW) {
+			gst[0] = xa_pack_state(p0[0], p1[0]);
+			gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
+		}
+		const bool more = S + 1 < NS;
+		if (more) {
+			if (S == 0)
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			else
+				wait_after(2 * S - 1);
+			take(0, nxt);
+			stage_half<BITS, CH>(a, land, lane, wstart, Cw, 1,
+			    rel_of(S + 1), voff);
+		}
+		asm volatile("" ::: "memory");
+		group(cur, S, std::integral_constant<int, 0>());
+		/* the staged lines have been read back */
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-		cur ^= 1;
+		if (more) {
+			wait_after(2 * S);
+			take(1, nxt);
+			if (S + 2 < NS)
+				stage_half<BITS, CH>(a, land, lane, wstart, Cw, 0,
+				    rel_of(S + 2), voff);
+		}
+		asm volatile("" ::: "memory");
+		group(cur, S, std::integral_constant<int, 1>());
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	};
+
+	uint32_t A[RD], B[RD];
+	/* prologue: super-step 0 into A, half 0 of super-step 1 in flight */
+	stage_half<BITS, CH>(a, land, lane, wstart, Cw, 0, rel_of(0), voff);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(0, A);
+	stage_half<BITS, CH>(a, land, lane, wstart, Cw, 1, rel_of(0), voff);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(1, A);
+	if (NS > 1)
+		stage_half<BITS, CH>(a, land, lane, wstart, Cw, 0, rel_of(1),
+		    voff);
+	for (int S = 0; S < NS; S += 2) {
+		step(S, A, B);
+		if (S + 1 < NS)
+			step(S + 1, B, A);
+	}
+	if (NS == NW) {	/* empty chunk (never planned) */
+		gst[0] = xa_pack_state(p0[0], p1[0]);
+		gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
 	}
 	if (chunk < a.nchunks) {
 		uint2 gv, ev;
@@ -571,16 +604,16 @@ spec_wave(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 
 /* K1 for one stream: wave w of the grid takes chunks 64w .. 64w+63 */
 template <int BITS, int CH, int LB, bool NT>
-__global__ __launch_bounds__(64 * XA_SPEC_WPB) void
+__global__ __launch_bounds__(64 * XA_SPEC_WPB, 8 / XA_SPEC_WPB) void
 xa_decode_spec(xa_dec_args a)
 {
-	typedef spec_lds<BITS, CH, LB> L;
-	__shared__ __attribute__((aligned(16))) uint8_t
-	    lds[XA_SPEC_WPB * 2 * L::REGION];
 	/* the wave index is wave-uniform; say so, so that LDS bases and the
 	 * DMA source base live in SGPRs */
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	spec_wave<BITS, CH, LB, NT, L::REGION>(a, lds + wv * 2 * L::REGION,
+	typedef spec_lds2<BITS, CH, LB> L;
+	__shared__ __attribute__((aligned(16))) uint8_t
+	    lds[XA_SPEC_WPB * L::REGION];
+	spec_wave2<BITS, CH, LB, NT>(a, lds + wv * L::REGION,
 	    blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u);
 }
 
@@ -657,8 +690,8 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 	int32_t p0, p1;
 	xa_unpack_state(sc, p0, p1);
 	const int64_t eblocks = a.eblocks;
-	const int64_t b0 = chunk_start<g::G>(a, q);
-	int64_t b1 = chunk_start<g::G>(a, q + 1);
+	const int64_t b0 = chunk_start<g::G2>(a, q);
+	int64_t b1 = chunk_start<g::G2>(a, q + 1);
 	if (b1 > eblocks)
 		b1 = eblocks;
 	const int64_t ndw = (eblocks * EBSZ + 3) / 4;
@@ -1091,20 +1124,22 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 
 template <int LB> struct batch_lds {
 	static constexpr int m(int x, int y) { return x > y ? x : y; }
-	static constexpr int REGION = m(m(m(spec_lds<8, 2, LB>::REGION,
-	    spec_lds<8, 1, LB>::REGION), m(spec_lds<6, 2, LB>::REGION,
-	    spec_lds<6, 1, LB>::REGION)), m(spec_lds<4, 2, LB>::REGION,
-	    spec_lds<4, 1, LB>::REGION));
+	/* one region per wave (landing buffer + output stage), the
+	 * largest over the formats */
+	static constexpr int REGION = m(m(m(spec_lds2<8, 2, LB>::REGION,
+	    spec_lds2<8, 1, LB>::REGION), m(spec_lds2<6, 2, LB>::REGION,
+	    spec_lds2<6, 1, LB>::REGION)), m(spec_lds2<4, 2, LB>::REGION,
+	    spec_lds2<4, 1, LB>::REGION));
 };
 
 /* K1 over a batch: wave w decodes 64 chunks of stream wstream[w] with that
  * stream's format (wave-uniform dispatch, no divergence) */
 template <int LB, bool NT>
-__global__ __launch_bounds__(64 * XA_SPEC_WPB) void
+__global__ __launch_bounds__(64 * XA_SPEC_WPB, 8 / XA_SPEC_WPB) void
 xa_decode_spec_batch(xa_batch_args b)
 {
-	constexpr int R = batch_lds<LB>::REGION;
-	__shared__ __attribute__((aligned(16))) uint8_t lds[XA_SPEC_WPB * 2 * R];
+	__shared__ __attribute__((aligned(16))) uint8_t
+	    lds[XA_SPEC_WPB * batch_lds<LB>::REGION];
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const uint32_t w = blockIdx.x * XA_SPEC_WPB + wv;
 	if (w >= b.nwaves)
@@ -1114,9 +1149,9 @@ xa_decode_spec_batch(xa_batch_args b)
 	const uint32_t fmt = __builtin_amdgcn_readfirstlane(b.streams[sid].fmt);
 	const uint32_t wchunk0 = 64u * w -
 	    __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
-	uint8_t *region = lds + wv * 2 * R;
+	uint8_t *region = lds + wv * batch_lds<LB>::REGION;
 	with_format(fmt, [&](auto bc, auto cc) {
-		spec_wave<decltype(bc)::value, decltype(cc)::value, LB, NT, R>(a,
+		spec_wave2<decltype(bc)::value, decltype(cc)::value, LB, NT>(a,
 		    region, wchunk0);
 	});
 }

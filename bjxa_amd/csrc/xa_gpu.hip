@@ -55,8 +55,8 @@ struct plan {
 /*
  * Chunk plan for one stream.  Automatic: uniform chunks (above).  With
  * XA_VARIANT_BALANCED: exactly TARGET_LANES chunks once the stream is long
- * enough, C = eblocks per lane rounded down to the group (G = 4/ch
- * eblocks) and the remainder spread as whole groups over the leading
+ * enough, C = eblocks per lane rounded down to the chunk quantum (G =
+ * XA_CHUNK_Q(ch) eblocks) and the remainder spread as whole quanta over the leading
  * chunks, rounded up to whole waves so every wave has one chunk length.
  * An explicit tune->chunk gives uniform chunks of that length.
  */
@@ -64,7 +64,7 @@ static void
 plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
     struct plan *p)
 {
-	const uint32_t G = 4 / ch;
+	const uint32_t G = XA_CHUNK_Q(ch);
 	const uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup :
 	    DEFAULT_WARMUP;
 	uint32_t c;
@@ -321,7 +321,8 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	}
 	uint64_t nwaves = 0;
 	for (uint32_t i = 0; i < n; i++) {
-		const uint32_t E = s[i].eblocks, ch = s[i].channels, G = 4 / ch;
+		const uint32_t E = s[i].eblocks, ch = s[i].channels,
+		    G = XA_CHUNK_Q(ch);
 		uint64_t k = ((uint64_t)E * ch + 32 * cb) / (64 * cb);
 		if (k == 0)
 			k = 1;
@@ -384,7 +385,7 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	a.wstream = (const uint32_t *)(ws + o_wav);
 	a.nstreams = n;
 	a.nwaves = (uint32_t)nwaves;
-	a.W = (w + 3) & ~3u;
+	a.W = (w + 7) & ~7u;	/* a whole chunk quantum of every format */
 	a.g = (uint2 *)(ws + o_g);
 	a.e = (uint2 *)(ws + o_e);
 	a.queue = (uint32_t *)(ws + o_q);

@@ -58,5 +58,7 @@ def test_auto_plan_ragged(built, bits, ch):
     got, st = dev_decode(xa, eb, bits, ch, frames=frames, state=(5, 6, -7, 8),
                          want_status=True)
     assert np.array_equal(got, ref)
-    assert st[6] == 20 and st[5] == -(-eb // 20)
+    q = 8 // ch                       # chunk quantum, eblocks (XA_CHUNK_Q)
+    c = -(-(-(-eb // 131072)) // q) * q
+    assert st[6] == c and st[5] == -(-eb // c)
     assert status_state(st)[:2 * ch] == st_ref[:2 * ch]

@@ -356,6 +356,147 @@ run_skel1(const uint8_t *src, uint8_t *dst, uint32_t lanes, uint32_t steps)
 	hipEventDestroy(b);
 }
 
+/*
+ * K1 skeleton with 264-B input runs: a lane's input for two steps (2 x 132
+ * B) arrives as one contiguous run, staged half a wave at a time through a
+ * single 32 x 272-B landing buffer and kept in VGPRs (two steps ahead), so
+ * each DMA instruction reads two ~264-B runs instead of seven 144-B ones.
+ * Output staging and stores as k_skel (8.5 + 9 KiB of LDS per wave).
+ */
+__global__ __launch_bounds__(256) void
+k_skel2(const uint8_t *src, uint8_t *dst, uint32_t steps)
+{
+	constexpr int RUN = 272, HALF = 32 * RUN, NI = (HALF + 1023) / 1024,
+	    LINE = 144, OS = 64 * LINE;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * (HALF + OS)];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *land = lds + wv * (HALF + OS), *ost = land + HALF;
+	const uint64_t w = blockIdx.x * 4u + wv;
+	const uint32_t CBI = steps * 132u, CBO = steps * 256u;
+	/* piece p of a half-wave landing image: run p / 17, offset p % 17 */
+	uint32_t voff[NI];
+#pragma unroll
+	for (int i = 0; i < NI; i++) {
+		const int k = i * 64 + lane;
+		voff[i] = (uint32_t)(k / 17) * CBI + (uint32_t)(k % 17) * 16u;
+	}
+	const uint8_t *wbi = src + w * 64ull * CBI;
+	const uint8_t *lim = src + (w + 1) * 64ull * CBI - 16;
+	uint8_t *wbo = dst + w * 64ull * CBO;
+	/* super-step S covers steps 2S, 2S+1 */
+	auto issue = [&](uint32_t S, int h) {
+		const uint8_t *b = wbi + (uint64_t)h * 32u * CBI + (uint64_t)S * 264u;
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			if (i == NI - 1 && lane >= (HALF / 16) - (NI - 1) * 64)
+				break;
+			const uint8_t *a = b + voff[i];
+			dma16(a < lim ? a : lim, land + i * 1024);
+		}
+	};
+	const uint32_t nS = steps / 2;
+	uint32_t cur[66], nxt[66];
+	auto take = [&](int h) {
+		if ((lane >> 5) == h) {
+			const uint32_t *m = (const uint32_t *)(land + (lane & 31) * RUN);
+#pragma unroll
+			for (int i = 0; i < 66; i++)
+				nxt[i] = m[i];
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	};
+	/* prologue: super-step 0 into cur */
+	issue(0, 0);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(0);
+	issue(0, 1);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(1);
+#pragma unroll
+	for (int i = 0; i < 66; i++)
+		cur[i] = nxt[i];
+	if (nS > 1)
+		issue(1, 0);
+	auto emit = [&](uint32_t s, const uint32_t *win) {
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			u32x4 v[8];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const int i = h * 32 + q * 4 + j;
+					v[q][j] = win[i % 33] ^ (uint32_t)i;
+				}
+			uint8_t *line = ost + lane * LINE;
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				*(u32x4 *)(line + q * 16) = v[q];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+			for (int i = 0; i < 8; i++) {
+				const int ln = i * 8 + lane / 8, pc = lane % 8;
+				const u32x4 x = *(const u32x4 *)(ost + ln * LINE + pc * 16);
+				uint8_t *o = wbo + (uint64_t)ln * CBO + s * 256u + h * 128u + pc * 16u;
+				__builtin_nontemporal_store(x, (u32x4 *)o);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+	};
+	for (uint32_t S = 0; S < nS; S++) {
+		const bool more = S + 1 < nS;
+		if (more) {
+			/* first half of S+1 landed (16 stores of step 2S-1 younger) */
+			if (S == 0)
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			take(0);
+			issue(S + 1, 1);
+		}
+		emit(2 * S, cur);
+		if (more) {
+			asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			take(1);
+			if (S + 2 < nS)
+				issue(S + 2, 0);
+		}
+		emit(2 * S + 1, cur + 33);
+#pragma unroll
+		for (int i = 0; i < 66; i++)
+			cur[i] = nxt[i];
+	}
+}
+
+static void
+run_skel2(const uint8_t *src, uint8_t *dst)
+{
+	const uint32_t lanes = 125056, steps = 20;
+	const unsigned grid = lanes / 256;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL(k_skel2, dim3(grid), dim3(256), 0, 0, src, dst, steps);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL(k_skel2, dim3(grid), dim3(256), 0, 0, src, dst, steps);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)lanes * steps * (132 + 256);
+	printf("{\"skel2\": 1, \"run\": 264, \"ms\": %.4f, \"TBs\": %.3f}\n", ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
 int
 main()
 {
@@ -379,10 +520,9 @@ main()
 	run_skel<true, false, true>(src, dst);
 	run_skel<false, true, true>(src, dst);
 	run_skel<false, false, true>(src, dst);
-	run_skel1(src, dst, 125184, 40);
-	run_skel1(src, dst, 187392, 27);
-	run_skel1(src, dst, 250112, 20);
-	run_skel1(src, dst, 62720, 80);
+	run_skel2(src, dst);
+	run_skel<true, true, true>(src, dst);
+	run_skel2(src, dst);
 	CHECK(hipDeviceSynchronize());
 	return 0;
 }
