@@ -448,7 +448,7 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 	int32_t p0[CH], p1[CH];
 #pragma unroll
 	for (int c = 0; c < CH; c++) {
-		if (b0 - W < 0)
+		if (b0 - W <= 0)	/* the stream start: the caller's state */
 			xa_unpack_state(a.init[c], p0[c], p1[c]);
 		else
 			p0[c] = p1[c] = 0;

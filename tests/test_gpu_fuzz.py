@@ -33,7 +33,7 @@ def case(rng, i):
     return xa, eb, bits, ch, eb * 32 - cut, state
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(16))
 def test_fuzz_single_stream(built, seed):
     rng = np.random.default_rng(100 + seed)
     for i in range(12):
@@ -54,7 +54,7 @@ def test_fuzz_single_stream(built, seed):
             assert np.array_equal(pcm[:n], ref[:n]), what
 
 
-@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("seed", range(6))
 def test_fuzz_batch(built, seed):
     rng = np.random.default_rng(200 + seed)
     specs = [case(rng, 1000 + seed * 100 + i) for i in range(int(rng.integers(1, 40)))]
