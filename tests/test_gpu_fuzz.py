@@ -62,3 +62,45 @@ def test_fuzz_batch(built, seed):
     warm = int(rng.choice([-1, 0, 5, 12]))
     pcms, st = run_batch(specs, chunk=chunk, warmup=warm)
     check(specs, pcms, st)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_host_api(built, seed):
+    """The unchanged bjxa_decode() on host buffers with random call sizes
+    (small-call path and bulk path, src/libbjxa.c:602-661 per call), the
+    state carried across calls, against one single-pass oracle decode."""
+    rng = np.random.default_rng(300 + seed)
+    bits, ch = FORMATS[seed % 6]
+    eb = int(rng.integers(1, 60_000))
+    frames = eb * 32 - int(rng.integers(0, 32))
+    state = tuple(int(v) for v in rng.integers(-32768, 32768, 4))
+    xa = synth.stream(eb, bits, ch, "AFWZ"[seed % 4], seed=7000 + seed)
+    ref, _, _, _ = oracle.decode(xa, eb, bits, ch, state, frames)
+    bx = (bits * 4 + 1) * ch
+    out = bytearray()
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(bjxa_amd.xa_header(xa.size, frames, 44100, bits, ch, state))
+        pos, left = 0, frames * ch * 2
+        while pos < eb:
+            n = min(int(np.exp(rng.uniform(0, np.log(20_000)))), eb - pos)
+            dst = np.zeros(n * 64 * ch, np.uint8)
+            assert d.decode(dst, xa[pos * bx:(pos + n) * bx].copy()) == n
+            take = min(n * 64 * ch, left)
+            out += dst[:take].tobytes()
+            left -= take
+            pos += n
+    assert bytes(out) == ref.tobytes()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_encode(built, seed):
+    """Device encode of random PCM lengths in every format against the
+    oracle's restatement of bjxa_encode (src/libbjxa.c:759-819)."""
+    from gpu_util import dev_encode
+    rng = np.random.default_rng(400 + seed)
+    for i in range(6):
+        bits, ch = FORMATS[int(rng.integers(0, 6))]
+        frames = int(np.exp(rng.uniform(0, np.log(2_000_000))))
+        pcm = synth.pcm(frames, ch, seed=seed * 10 + i)
+        assert np.array_equal(dev_encode(pcm, frames, bits, ch),
+                              oracle.encode(pcm, frames, bits, ch)), (seed, i, bits, ch, frames)
