@@ -497,6 +497,145 @@ run_skel2(const uint8_t *src, uint8_t *dst)
 	hipEventDestroy(b);
 }
 
+/*
+ * Generalised run skeleton: runs of NG groups (NG x 132 B), landed by
+ * 64/NG lanes at a time (NG sub-phases per super-step, one group decoded
+ * per sub-phase), WPB waves per workgroup and a caller-chosen grid (so the
+ * occupancy can drop to one wave per SIMD, where NG = 4 fits the VGPRs).
+ */
+template <int NG, int WPB>
+__global__ __launch_bounds__(64 * WPB, 1) void
+k_skelN(const uint8_t *src, uint8_t *dst, uint32_t steps)
+{
+	constexpr int RUNB = NG * 132, RUN = (RUNB + 15) / 16 * 16, LANES = 64 / NG,
+	    IMG = LANES * RUN, NPR = RUN / 16, NI = (LANES * NPR + 63) / 64,
+	    LASTL = LANES * NPR - 64 * (NI - 1), LINE = 144, OS = 64 * LINE, RD = NG * 33;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[WPB * (IMG + OS)];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *land = lds + wv * (IMG + OS), *ost = land + IMG;
+	const uint64_t w = blockIdx.x * (uint64_t)WPB + wv;
+	const uint32_t CBI = steps * 132u, CBO = steps * 256u;
+	uint32_t voff[NI];
+#pragma unroll
+	for (int i = 0; i < NI; i++) {
+		const int k = i * 64 + lane;
+		voff[i] = (uint32_t)(k / NPR) * CBI + (uint32_t)(k % NPR) * 16u;
+	}
+	const uint8_t *wbi = src + w * 64ull * CBI;
+	const uint8_t *lim = src + (w + 1) * 64ull * CBI - 16;
+	uint8_t *wbo = dst + w * 64ull * CBO;
+	auto issue = [&](uint32_t S, int h) {
+		const uint8_t *b = wbi + (uint64_t)h * LANES * CBI + (uint64_t)S * RUNB;
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			if (i == NI - 1 && lane >= LASTL)
+				break;
+			const uint8_t *a = b + voff[i];
+			dma16(a < lim ? a : lim, land + i * 1024);
+		}
+	};
+	const uint32_t nS = steps / NG;
+	uint32_t A[RD], B[RD];
+	auto take = [&](int h, uint32_t *d) {
+		if (lane / LANES == h) {
+			const uint32_t *m = (const uint32_t *)(land + (lane % LANES) * RUN);
+#pragma unroll
+			for (int i = 0; i < RD; i++)
+				d[i] = m[i];
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	};
+	auto emit = [&](uint32_t s, const uint32_t *win) {
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			u32x4 v[8];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const int i = h * 32 + q * 4 + j;
+					v[q][j] = win[i % 33] ^ (uint32_t)i;
+				}
+			uint8_t *line = ost + lane * LINE;
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				*(u32x4 *)(line + q * 16) = v[q];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+			for (int i = 0; i < 8; i++) {
+				const int ln = i * 8 + lane / 8, pc = lane % 8;
+				const u32x4 x = *(const u32x4 *)(ost + ln * LINE + pc * 16);
+				uint8_t *o = wbo + (uint64_t)ln * CBO + s * 256u + h * 128u + pc * 16u;
+				__builtin_nontemporal_store(x, (u32x4 *)o);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+	};
+	/* prologue: super-step 0 into A, sub-phase 0 of super-step 1 in flight */
+#pragma unroll
+	for (int h = 0; h < NG; h++) {
+		issue(0, h);
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		take(h, A);
+	}
+	if (nS > 1)
+		issue(1, 0);
+	auto step = [&](uint32_t S, uint32_t *cur, uint32_t *nxt) {
+		const bool more = S + 1 < nS;
+#pragma unroll
+		for (int h = 0; h < NG; h++) {
+			if (more) {
+				if (S == 0 && h == 0)
+					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				else
+					asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+				take(h, nxt);
+				if (h + 1 < NG)
+					issue(S + 1, h + 1);
+				else if (S + 2 < nS)
+					issue(S + 2, 0);
+			}
+			asm volatile("" ::: "memory");
+			emit(S * NG + h, cur + h * 33);
+		}
+	};
+	for (uint32_t S = 0; S < nS; S += 2) {
+		step(S, A, B);
+		if (S + 1 < nS)
+			step(S + 1, B, A);
+	}
+}
+
+template <int NG, int WPB>
+static void
+run_skelN(const uint8_t *src, uint8_t *dst, uint32_t lanes, uint32_t steps)
+{
+	const unsigned grid = lanes / (64 * WPB);
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL((k_skelN<NG, WPB>), dim3(grid), dim3(64 * WPB), 0, 0, src, dst, steps);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL((k_skelN<NG, WPB>), dim3(grid), dim3(64 * WPB), 0, 0, src, dst, steps);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)grid * 64 * WPB * steps * (132 + 256);
+	printf("{\"skelN\": %d, \"wpb\": %d, \"lanes\": %u, \"steps\": %u, \"wgs\": %u, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    NG, WPB, grid * 64 * WPB, steps, grid, ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
 int
 main()
 {
@@ -520,8 +659,12 @@ main()
 	run_skel<true, false, true>(src, dst);
 	run_skel<false, true, true>(src, dst);
 	run_skel<false, false, true>(src, dst);
-	run_skel2(src, dst);
 	run_skel<true, true, true>(src, dst);
+	run_skel2(src, dst);
+	run_skelN<2, 4>(src, dst, 125440, 20);
+	run_skelN<4, 4>(src, dst, 62720, 40);
+	run_skelN<4, 4>(src, dst, 125440, 20);
+	run_skelN<2, 4>(src, dst, 62720, 40);
 	run_skel2(src, dst);
 	CHECK(hipDeviceSynchronize());
 	return 0;
