@@ -100,6 +100,8 @@ _SIGS = {
     "bjxa_hip_batch_decode_async": (ctypes.c_int, [_P, _P, _P, _P]),
     "bjxa_hip_batch_free": (None, [_P]),
     "bjxa_hip_decode_files": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint32]),
+    # LIBBJXA_HIP_0.2
+    "bjxa_hip_parse_headers_async": (ctypes.c_int, [_P, _SZ, ctypes.c_uint32, _P, _P]),
 }
 REFERENCE_SYMBOLS = {  # src/libbjxa.map:16-47
     "LIBBJXA_0.1": ["bjxa_decode", "bjxa_decode_format", "bjxa_decoder", "bjxa_dump_pcm",
@@ -113,7 +115,8 @@ EXTENSION_SYMBOLS = {"LIBBJXA_HIP_0.1": ["bjxa_hip_batch_decode_async", "bjxa_hi
                                          "bjxa_hip_batch_new", "bjxa_hip_decode_async",
                                          "bjxa_hip_decode_files",
                                          "bjxa_hip_decode_workspace", "bjxa_hip_encode_async",
-                                         "bjxa_hip_version", "bjxa_hip_workspace_init"]}
+                                         "bjxa_hip_version", "bjxa_hip_workspace_init"],
+                     "LIBBJXA_HIP_0.2": ["bjxa_hip_parse_headers_async"]}
 
 
 def lib():
@@ -378,6 +381,21 @@ def parse_header_fields(data):
     data_len, samples, rate, bits, ch = struct.unpack("<IIHBB", bytes(data[4:16]))
     return {"data_len": data_len, "samples": samples, "rate": rate, "bits": bits,
             "channels": ch}
+
+
+def header_record():
+    """numpy dtype of bjxa_hip_header_t (include/bjxa_hip.h), 32 bytes."""
+    import numpy as np
+    return np.dtype([("data_len", "<u4"), ("samples", "<u4"), ("blocks", "<u4"),
+                     ("data_len_pcm", "<u4"), ("rate", "<u2"), ("bits", "u1"),
+                     ("channels", "u1"), ("state", "<i2", 4), ("status", "<i4")])
+
+
+def parse_headers_device(d_src, stride, n, d_out, stream=0):
+    """Validate n device-resident XA headers (bjxa_parse_header's checks,
+    src/libbjxa.c:395-453) into n header_record() entries at d_out."""
+    _check(lib().bjxa_hip_parse_headers_async(d_src, stride, n, d_out, stream),
+           "bjxa_hip_parse_headers_async")
 
 
 def encode_device(d_pcm, frames, bits, channels, d_xa, stream=0):

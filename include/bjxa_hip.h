@@ -107,6 +107,30 @@ int bjxa_hip_decode_files(const void *const *xa, const size_t *xa_len,
 int bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
     unsigned channels, void *d_xa, void *stream);
 
+/*
+ * Validate n XA headers held in device memory (32 bytes each, header i at
+ * d_src + i * stride; any alignment) with the checks, order and uint32
+ * arithmetic of bjxa_parse_header (src/libbjxa.c:395-453), one thread per
+ * header, and write one record each (LIBBJXA_HIP_0.2).  A stereo header
+ * whose payload is an odd number of channel blocks passes the reference's
+ * checks and then trips its format assertion (:597); here it is EPROTO.
+ * For batches of files already in HBM (10^5 and more).
+ */
+typedef struct {
+	uint32_t	data_len;	/* XA block bytes (nDataLen) */
+	uint32_t	samples;	/* frames (nSamples) */
+	uint32_t	blocks;		/* effective blocks */
+	uint32_t	data_len_pcm;	/* samples * channels * 2 */
+	uint16_t	rate;
+	uint8_t		bits;
+	uint8_t		channels;
+	int16_t		state[4];	/* befL[0..1], befR[0..1] */
+	int32_t		status;		/* 0 or EPROTO; the rest is 0 on EPROTO */
+} bjxa_hip_header_t;		/* 32 bytes */
+
+int bjxa_hip_parse_headers_async(const void *d_src, size_t stride, uint32_t n,
+    bjxa_hip_header_t *d_out, void *stream);
+
 /* library/kernels build identifier, e.g. "bjxa-mi355x gfx950 ..." */
 const char *bjxa_hip_version(void);
 

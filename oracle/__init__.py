@@ -69,6 +69,76 @@ def parse_xa_header(buf):
                 bits=bits, channels=ch, state=(l0, l1, r0, r1))
 
 
+def validate_xa_header(buf):
+    """bjxa_parse_header's checks (src/libbjxa.c:405-437, in that order,
+    uint32 arithmetic) and bjxa_decode_format's block count (:588-597).
+    Returns None on EPROTO -- including a stereo payload of an odd number of
+    channel blocks, which passes :425-437 and trips the assertion at :597 --
+    else the fields of a bjxa_hip_header_t record."""
+    h = parse_xa_header(buf)
+    dl, ns, bits, ch = h["data_len"], h["samples"], h["bits"], h["channels"]
+    if h["magic"] != b"KWD1" or dl == 0 or ns == 0 or h["rate"] == 0:
+        return None
+    if bits not in (4, 6, 8) or ch not in (1, 2):
+        return None
+    bs = bits * 4 + 1
+    max_samples = ((32 * dl) & 0xffffffff) // (bs * ch)
+    if (dl // bs) * bs != dl or max_samples < ns or max_samples - ns >= 32:
+        return None
+    blocks = dl // (bs * ch)
+    if blocks * bs * ch != dl:
+        return None
+    return dict(data_len=dl, samples=ns, blocks=blocks,
+                data_len_pcm=(ns * ch * 2) & 0xffffffff, rate=h["rate"], bits=bits,
+                channels=ch, state=h["state"])
+
+
+def random_xa_headers(rng, n):
+    """n 32-byte XA headers, about half valid, the rest broken in one of the
+    ways the checks of src/libbjxa.c:405-437 catch (test input generator)."""
+    out = np.zeros((n, 32), np.uint8)
+    for i in range(n):
+        bits = int(rng.choice([4, 6, 8]))
+        ch = int(rng.integers(1, 3))
+        bs = bits * 4 + 1
+        nblk = int(np.exp(rng.uniform(0, np.log(2e8 / bs))))
+        if ch == 2 and rng.random() < 0.8:
+            nblk += nblk & 1
+        dl = nblk * bs
+        mx = ((32 * dl) & 0xffffffff) // (bs * ch)
+        ns = max(1, mx - int(rng.integers(0, 32)))
+        rate = int(rng.choice([22050, 44100, 48000, 1]))
+        magic = b"KWD1"
+        state = [int(v) for v in rng.integers(-32768, 32768, 4)]
+        k = int(rng.integers(0, 14))
+        if k == 0:
+            magic = b"KWD" + bytes([int(rng.integers(0, 256))])
+        elif k == 1:
+            dl = 0
+        elif k == 2:
+            ns = 0
+        elif k == 3:
+            rate = 0
+        elif k == 4:
+            bits = int(rng.choice([0, 1, 5, 7, 9, 16, 255]))
+        elif k == 5:
+            ch = int(rng.choice([0, 3, 4, 255]))
+        elif k == 6:
+            dl += int(rng.integers(1, bs))
+        elif k == 7:
+            ns = mx + int(rng.integers(1, 100))
+        elif k == 8:
+            ns = max(1, mx - int(rng.integers(32, 1000)))
+        elif k == 9:
+            dl = int(rng.integers(1, 2**32))
+            ns = int(rng.integers(1, 2**32))
+        out[i] = np.frombuffer(magic + struct.pack("<IIHBBIhhhhI", dl & 0xffffffff,
+                               ns & 0xffffffff, rate, bits & 0xff, ch & 0xff,
+                               int(rng.integers(0, 2**32)), *state,
+                               int(rng.integers(0, 2**32))), np.uint8)
+    return out
+
+
 def riff_header(ch, rate, data_len_pcm):
     """44-byte RIFF/WAVE header (bjxa_dump_riff_header, src/libbjxa.c:898-927)."""
     return (b"RIFF" + struct.pack("<I", 36 + data_len_pcm) + b"WAVEfmt " +
