@@ -511,9 +511,11 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 			const int64_t b = b0 + s0 + u;
 			auto flush = [&](int h) {
 				wave_lds_sync();
+				__builtin_amdgcn_s_setprio(1);
 				store_lines<LB, NT>(a, ost, lane, wchunk0, wstart_b,
 				    chunk_bytes, (uint32_t)s0 * OB + (uint32_t)LB * h,
 				    wave_full, clean, gbase, lbase);
+				__builtin_amdgcn_s_setprio(0);
 				wave_lds_sync();
 			};
 			const bool act = b < eblocks;
@@ -539,6 +541,14 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 		sfor<0, G>::run(body);
 	};
 
+	/* wave priority: a wave that has its next run landed takes the issue
+	 * slot for its LDS reads and DMA ahead of the other wave's decode VALU
+	 * (2), and for its PCM stores (1), so the memory pipeline sees the
+	 * next requests sooner (C3 spec -1.3 %, C2 -1.6 %; the stores above
+	 * or level with the DMA measured no better than without priorities) */
+	auto prio = [](auto pc) {
+		__builtin_amdgcn_s_setprio(decltype(pc)::value);
+	};
 	/* one super-step from run `cur`, landing the next one into `nxt` */
 	auto step = [&](int S, uint32_t *cur, uint32_t *nxt) {
 		if (S == NW) {
@@ -551,9 +561,11 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 			else
 				wait_after(2 * S - 1);
+			prio(std::integral_constant<int, 2>());
 			take(0, nxt);
 			stage_half<BITS, CH>(a, land, lane, wstart, Cw, 1,
 			    rel_of(S + 1), voff);
+			prio(std::integral_constant<int, 0>());
 		}
 		asm volatile("" ::: "memory");
 		group(cur, S, std::integral_constant<int, 0>());
@@ -561,10 +573,12 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		if (more) {
 			wait_after(2 * S);
+			prio(std::integral_constant<int, 2>());
 			take(1, nxt);
 			if (S + 2 < NS)
 				stage_half<BITS, CH>(a, land, lane, wstart, Cw, 0,
 				    rel_of(S + 2), voff);
+			prio(std::integral_constant<int, 0>());
 		}
 		asm volatile("" ::: "memory");
 		group(cur, S, std::integral_constant<int, 1>());
