@@ -13,9 +13,9 @@ for r in 1 2; do
 for v in $VARIANTS; do
   export BJXA_LIB_PATH=$R/dbg/$v/libbjxa.so.0
   for w in $WL; do
-    timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/ab_${v}_${w}_$r" -o run \
-        -- python3 "$R/bench.py" --no-cpu --no-other --steps 200 --workload $w \
-        > "$R/gpurun_out/ab_${v}_${w}_$r.log" 2>&1
+    timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/ab_${v}_${w}${MIX}_$r" -o run \
+        -- python3 "$R/bench.py" --no-cpu --no-other --steps 200 --workload $w --mix ${MIX:-A} \
+        > "$R/gpurun_out/ab_${v}_${w}${MIX}_$r.log" 2>&1
   done
 done
 done
