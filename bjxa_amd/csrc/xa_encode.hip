@@ -82,6 +82,10 @@ xa_encode_waves(xa_enc_args a)
 	/* stage: DMA instruction i, lane t fills position t % 16 of row
 	 * 4i + t / 16 with piece (t % 16) ^ (row & 15) of that row */
 	const uint64_t lastp = (pcm_bytes - 1) & ~(uint64_t)15;
+	/* wave priority: a starting wave issues its DMA ahead of the other
+	 * waves' packing VALU (2), its stores next (1): 168.0 -> 166.2 us on
+	 * C3-shaped PCM, one box */
+	__builtin_amdgcn_s_setprio(2);
 #pragma unroll
 	for (int i = 0; i < 16; i++) {
 		const int row = 4 * i + (lane >> 4);
@@ -92,6 +96,7 @@ xa_encode_waves(xa_enc_args a)
 		__builtin_amdgcn_global_load_lds(a.src + off, LDS_PTR(buf + i * 1024),
 		    16, 0, 0);
 	}
+	__builtin_amdgcn_s_setprio(0);
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	wave_sync();
 
@@ -134,6 +139,7 @@ xa_encode_waves(xa_enc_args a)
 	const uint64_t valid = nxa - ostart < (uint64_t)NOUT ? nxa - ostart :
 	    (uint64_t)NOUT;
 	if (valid == (uint64_t)NOUT && ((uintptr_t)dst & 15u) == 0) {
+		__builtin_amdgcn_s_setprio(1);
 #pragma unroll
 		for (int i = 0; i < (NOUT / 16 + 63) / 64; i++) {
 			const int k = 64 * i + lane;
