@@ -694,7 +694,7 @@ pair_swap(uint32_t v)
  * loads): the next block's window and old end state are fetched every
  * iteration with clamped addresses, one block ahead.
  */
-template <int BITS, int CH>
+template <int BITS, int CH, bool BUF = false>
 __device__ bool
 fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 {
@@ -712,11 +712,32 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 	const uint32_t *src = (const uint32_t *)a.src;
 
 	uint32_t raw[WN + 1], nraw[WN + 1];
+	/* BUF (one stream per launch, under 4 GiB of XA): the window comes
+	 * through a buffer descriptor of the stream, whose range check
+	 * returns 0 past the end, so the per-dword 64-bit clamps (about 90 of
+	 * the ~530 instructions a repaired block issues) go away */
+	__amdgpu_buffer_rsrc_t rs;
+	if constexpr (BUF) {
+		const uint64_t sp = (uint64_t)a.src;
+		const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)sp);
+		const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(sp >> 32));
+		const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)(ndw * 4));
+		rs = __builtin_amdgcn_make_buffer_rsrc(
+		    (void *)(((uint64_t)hi << 32) | lo), 0, (int)nb, 0x00020000);
+	}
 	auto fetch = [&](uint32_t *r, int64_t b) {
 		const int64_t d0 = (b * EBSZ + c * BSZ) >> 2;
+		if constexpr (BUF) {
+			const uint32_t o = (uint32_t)d0 * 4u;
 #pragma unroll
-		for (int i = 0; i <= WN; i++)
-			r[i] = src[min(d0 + i, ndw - 1)];
+			for (int i = 0; i <= WN; i++)
+				r[i] = __builtin_amdgcn_raw_buffer_load_b32(rs,
+				    (int)(o + 4u * i), 0, 0);
+		} else {
+#pragma unroll
+			for (int i = 0; i <= WN; i++)
+				r[i] = src[min(d0 + i, ndw - 1)];
+		}
 	};
 	/* old end state (frames 30, 31) of channel c of block b */
 	auto old_state = [&](int64_t b) -> uint32_t {
@@ -879,7 +900,7 @@ heap_pop(uint32_t *h, uint32_t &n)
  * bookkeeping), then publish the status words and reset the control words.
  * Queue entries are >= 1, so 0 ends the loop.
  */
-template <int BITS, int CH>
+template <int BITS, int CH, bool BUF>
 __device__ void
 drain_tail(const xa_dec_args &a)
 {
@@ -901,7 +922,7 @@ drain_tail(const xa_dec_args &a)
 			continue;
 		tail++;
 		uint2 ex;
-		const bool met = fix_lane<BITS, CH>(a, q, c, c ? s.y : s.x, ex);
+		const bool met = fix_lane<BITS, CH, BUF>(a, q, c, c ? s.y : s.x, ex);
 		if (c == 0) {
 			a.g[q] = s;
 			if (!met && q + 1 < a.nchunks)
@@ -940,7 +961,7 @@ drain_tail(const xa_dec_args &a)
 #define XA_FIX_CPT 2
 #endif
 
-template <int BITS, int CH>
+template <int BITS, int CH, bool BUF>
 __global__ __launch_bounds__(256) void
 xa_decode_fix(xa_dec_args a)
 {
@@ -987,7 +1008,7 @@ xa_decode_fix(xa_dec_args a)
 			const uint32_t q = fixq[k];
 			const uint2 s = fixs[k];
 			uint2 ex;
-			const bool met = fix_lane<BITS, CH>(a, q, c, c ? s.y : s.x,
+			const bool met = fix_lane<BITS, CH, BUF>(a, q, c, c ? s.y : s.x,
 			    ex);
 			wrote = true;
 			if (c != 0)
@@ -1021,7 +1042,7 @@ xa_decode_fix(xa_dec_args a)
 	/* acquire: this CU now sees every other workgroup's writes */
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	drain_tail<BITS, CH>(a);
+	drain_tail<BITS, CH, BUF>(a);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1056,8 +1077,19 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
 #if !defined(XA_DBG_STEP) && !defined(XA_DBG_NOSTORE) && !defined(XA_DBG_CONTIG)
-	hipLaunchKernelGGL((xa_decode_fix<BITS, CH>), dim3(grid2), dim3(256), 0,
-	    st, a);
+#ifdef XA_FIX_NOBUF
+	const bool buf = false;
+#else
+	/* buffer-descriptor windows need 32-bit byte offsets */
+	const bool buf = (uint64_t)a.eblocks * geo<BITS, CH>::EBSZ <
+	    (1ull << 32) - 256u;
+#endif
+	if (buf)
+		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, true>), dim3(grid2),
+		    dim3(256), 0, st, a);
+	else
+		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, false>), dim3(grid2),
+		    dim3(256), 0, st, a);
 #endif
 	return hipGetLastError();
 }
