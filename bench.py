@@ -1,40 +1,60 @@
 #!/usr/bin/env python3
 """bench.py -- XA ADPCM decode throughput on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path (bjxa_hip_decode_async: speculative
-decode + verify/repair/tail) over one synthetic XA stream already resident
-in HBM.  The bench line is BASELINE config C3 -- one 8-bit stereo stream of
-5,000,000 effective blocks (320M int16 samples), profile mix A -- the case
-north_star quotes its target on; at N=1 the same run also measures C2
-(configs[1]: one 8-bit mono stream of 10,000,000 blocks) and the batched
-configs C4 (1024 mixed-format streams per launch) and C5g (one GPU's share of
-C5 at 8 GPUs), and the encode direction on C3-shaped PCM, reported under
-"other_configs" (--no-other skips them).
+One step = one pass of the hot path over one synthetic input already
+resident in HBM.
 
-Multi-GPU (torchrun, one process per GPU): every rank decodes its own
-C3-sized stream (independent objects, no data-path collective), so per-GPU
-work is fixed: "scaling": "weak".  RCCL carries only the barriers, the max
-over ranks of the timed region and the AND of the bit-exact checks.
+N = 1 (default): BASELINE config C3 -- one 8-bit stereo stream of 5,000,000
+effective blocks (320M int16 samples), profile mix A, decoded by
+bjxa_hip_decode_async (speculative decode + verify/repair/tail).  The same
+run measures, under "other_configs": C2 (one 8-bit mono stream of 10M
+blocks), C4 (1024 mixed-format streams per launch), C5 (the whole 1024-stream
+job on this GPU: the N = 1 point of the scaling curve), C5g (one GPU's share
+of C5 at 8 GPUs) and the encode direction on C3-shaped PCM.  --no-other
+skips them.
+
+N > 1 (`--gpus N`): BASELINE config C5 -- 1024 8-bit stereo streams of
+65,536 eblocks, a fixed job split into contiguous shares, one rank per GPU,
+one batched launch per rank per step: "scaling": "strong".  Without
+WORLD_SIZE in the environment, bench.py starts the N ranks itself (a child
+`torch.distributed.run`, before anything touches the GPU) and passes its
+exit status through; under torchrun it is one of the ranks.  The data path
+has no collective (streams are independent); RCCL carries the control plane
+of SURVEY.md §5: the barriers, the max over ranks of the timed region,
+AllReduce(sum) of the counters, AllReduce(min) of the first failing stream,
+and an AllGather of every stream's 64-bit PCM checksum, which rank 0 checks
+against the oracle's.  C3 on every rank (weak scaling) is reported under
+other_configs.
 
 Reported:
-  value       decoded MSamples/s of the whole job (all ranks) over the timed
-              steps (barrier + synchronize on both sides, max over ranks)
-  roofline    xa_decode_spec, the dominant kernel: algorithmic bytes per
-              launch (XA read + PCM written, SURVEY.md §8(d): 3.03125 B per
-              8-bit sample) / its mean duration from hipEvents recorded on
-              the launch stream (every EV_EVERY-th timed step), against
-              8 TB/s; the read-only fraction
-              beside it; traffic = HBM bytes per launch from the committed
-              rocprofv3 PMC summary (profiles/pmc_latest.json)
-  cpu_baseline  the oracle (CPU restatement of libbjxa's decode, 1 thread)
-              on the same stream, rank 0 at N=1 only: median of 5 passes
-              after a discarded first pass (the bit-exact check)
+  value       decoded MSamples/s of the whole job over the timed steps
+              (barrier + synchronize on both sides, max over ranks)
+  roofline    the dominant kernel (xa_decode_spec; xa_decode_spec_batch for
+              C5): algorithmic bytes per launch (XA read + PCM written,
+              SURVEY.md §8(d): 3.03125 B per 8-bit sample) / its median
+              duration over >= 20 launches timed with hipEvents recorded on
+              the launch stream in a separate pass after the timed region,
+              against 8 TB/s; the read-only fraction beside it; traffic =
+              HBM bytes per launch from the committed rocprofv3 PMC summary
+              (profiles/pmc_latest.json) when it was taken on this workload
+  cpu_baseline  rank 0 at N = 1: the oracle (CPU restatement of libbjxa's
+              decode): C2/C3 on 1 thread (the stream is serial), C4/C5 on
+              all host cores the process may use (capped at 16, the box's
+              share), one decoder per thread, streams round-robin; median of
+              5 passes after a discarded first
+
+CPU rehearsal: BJXA_BENCH_BACKEND=gloo runs the N > 1 path on CPU (gloo,
+small job via --streams/--eblocks), decoding each rank's share with the
+library's host API on its CPU core; tests/test_dist.py drives it.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -47,12 +67,41 @@ WORKLOADS = {
     "C2": (10_000_000, 8, 1, "C2: 8-bit mono XA stream, 10,000,000 blocks"),
     "C3": (5_000_000, 8, 2, "C3: 8-bit stereo XA stream, 5,000,000 eblocks"),
 }
+BATCHES = {
+    # SURVEY.md §8(d): C4 = 1024 mixed-format streams; C5 = 1024 8-bit stereo
+    # streams of 65,536 eblocks over 1-8 GPUs -- "C5g" is one GPU's share at 8
+    "C4": "C4: 1024 streams, bits (4,6,8)[i%3], channels 1+((i/3)&1), 16,384 eblocks each",
+    "C5": "C5: 1024 8-bit stereo streams of 65,536 eblocks, a contiguous share per rank",
+    "C5g": "C5 per-GPU share at 8 GPUs: 128 8-bit stereo streams of 65,536 eblocks",
+}
+METRIC = "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 CPU_PASSES = 5
-# hipEvent pairs around the spec kernel are recorded on every EV_EVERY-th
-# timed step only: a timing event drains the stream (measured +5.5 us per
-# step when recorded on every step)
-EV_EVERY = 5
+EV_SAMPLES = 20         # launches timed with events, after the timed region
+CPU_THREADS_CAP = 16    # a GPU box's CPU share per GPU
+NO_ERROR = 0xFFFFFFFF
+FIRST_ERR_NONE = (1 << 62)
+
+
+# ---- process plumbing --------------------------------------------------------
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Start n ranks of this script under torch.distributed.run (one process
+    per GPU) from a parent that has not touched the GPU, and return their
+    exit status.  The ranks' stdout (rank 0's JSON line) passes through."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % n, "--master-addr=127.0.0.1",
+           "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def hip_runtime():
@@ -66,10 +115,38 @@ def hip_runtime():
     return L
 
 
+class EventPairs:
+    """hipEvent pairs recorded around the spec kernel on the launch stream
+    (torch.cuda.Event only sees torch's current stream)."""
+
+    def __init__(self, n):
+        self.hip = hip_runtime()
+        self.ev = []
+        for _ in range(n):
+            a, b = ctypes.c_void_p(), ctypes.c_void_p()
+            self.hip.hipEventCreate(ctypes.byref(a))
+            self.hip.hipEventCreate(ctypes.byref(b))
+            self.ev.append((a.value, b.value))
+
+    def ms(self):
+        out = []
+        for a, b in self.ev:
+            f = ctypes.c_float()
+            self.hip.hipEventSynchronize(b)
+            self.hip.hipEventElapsedTime(ctypes.byref(f), a, b)
+            out.append(f.value)
+        return out
+
+    def close(self):
+        for a, b in self.ev:
+            self.hip.hipEventDestroy(a)
+            self.hip.hipEventDestroy(b)
+
+
 def reduce_over_ranks(elapsed, ok, dev):
     """Whole-job view of one rank's result: the max of the timed region over
     ranks and the AND of the bit-exact checks (None = not checked counts as
-    passing).  RCCL on the GPU box; the gloo test runs it on CPU tensors."""
+    passing).  RCCL on the GPU box; the gloo tests run it on CPU tensors."""
     import torch
     import torch.distributed as dist
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -80,7 +157,7 @@ def reduce_over_ranks(elapsed, ok, dev):
 
 
 def job_value(samples_per_rank, world, steps, elapsed):
-    """MSamples/s of the whole job: every rank decodes its own stream."""
+    """MSamples/s of a weak-scaling job: every rank decodes its own stream."""
     return samples_per_rank * world * steps / elapsed / 1e6
 
 
@@ -95,9 +172,40 @@ def host_cpu():
     return "unknown"
 
 
+def cpu_threads():
+    """Host cores this process may use, capped at the box's per-GPU share."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, CPU_THREADS_CAP)), os.cpu_count()
+
+
+# ---- PCM checksums (the AllGather payload) -------------------------------------
+
+def pcm_checksum_np(pcm_i16):
+    """64-bit position-weighted checksum of an int16 PCM array (wrapping
+    int64 arithmetic, so any summation order gives the same value)."""
+    x = pcm_i16.astype(np.int64)
+    w = (np.arange(x.size, dtype=np.int64) % 65521) + 1
+    with np.errstate(over="ignore"):
+        return int(np.sum(x * w, dtype=np.int64))
+
+
+def pcm_checksum_torch(buf_u8, n):
+    """The same checksum of the first n int16 of a device byte buffer."""
+    import torch
+    x = buf_u8[:2 * n].view(torch.int16).to(torch.int64)
+    w = torch.arange(n, dtype=torch.int64, device=x.device) % 65521 + 1
+    return int((x * w).sum().item())
+
+
+# ---- one long stream per rank (C2/C3) ----------------------------------------
+
 def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     """Decode one seeded stream `args.steps` times (after `args.warmup`
-    untimed steps); returns the measurements of this rank."""
+    untimed steps), then time EV_SAMPLES more launches with events;
+    returns the measurements of this rank."""
     import torch
     import torch.distributed as dist
     import bjxa_amd
@@ -114,48 +222,30 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     sh = torch.cuda.current_stream(dev).cuda_stream
     bjxa_amd.workspace_init(ws.data_ptr(), ws_len, sh)
 
-    hip = hip_runtime()
-    nev = args.steps + args.warmup
-    evs = []
-    for _ in range(nev):
-        a, b = ctypes.c_void_p(), ctypes.c_void_p()
-        hip.hipEventCreate(ctypes.byref(a))
-        hip.hipEventCreate(ctypes.byref(b))
-        evs.append((a.value, b.value))
-
-    def step(i):
-        ev = evs[i] if (i - args.warmup) % EV_EVERY == 0 else (None, None)
+    def step(ev=(None, None)):
         bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, bits, ch,
                                ws.data_ptr(), ws_len, status.data_ptr(), (0, 0, 0, 0),
                                args.chunk, args.warm_blocks, sh, ev)
 
-    for i in range(args.warmup):
-        step(i)
+    for _ in range(args.warmup):
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.warmup, nev):
-        step(i)
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = t1 - t0
 
-    spec_ms = []
-    for i in range(args.warmup, nev):
-        if (i - args.warmup) % EV_EVERY:
-            continue
-        a, b = evs[i]
-        ms = ctypes.c_float()
-        hip.hipEventSynchronize(b)
-        hip.hipEventElapsedTime(ctypes.byref(ms), a, b)
-        spec_ms.append(ms.value)
-    for a, b in evs:
-        hip.hipEventDestroy(a)
-        hip.hipEventDestroy(b)
+    evs = EventPairs(max(EV_SAMPLES, args.steps))
+    for ev in evs.ev:
+        step(ev)
+    spec_ms = evs.ms()
+    evs.close()
     st = status.cpu().numpy().view(np.uint32).copy()
 
     ok, cpu = None, None
@@ -181,26 +271,21 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
 
     xa_bytes = eb * ch * (bits * 4 + 1)
     return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
-            "elapsed": elapsed, "spec_ms": float(np.mean(spec_ms)), "status": st,
-            "xa_bytes": xa_bytes, "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
+            "elapsed": elapsed, "spec_ms": float(np.median(spec_ms)),
+            "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
+            "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
 
 
-BATCHES = {
-    # SURVEY.md §8(d): C4 = 1024 mixed-format streams; C5 = 1024 8-bit stereo
-    # streams of 65,536 eblocks over 8 GPUs -- "C5g" is one GPU's share
-    "C4": "C4: 1024 streams, bits (4,6,8)[i%3], channels 1+((i/3)&1), 16,384 eblocks each",
-    "C5g": "C5 per-GPU share at 8 GPUs: 128 8-bit stereo streams of 65,536 eblocks",
-    "C5": "C5: 1024 8-bit stereo streams of 65,536 eblocks, a contiguous share per rank",
-}
+# ---- batched streams (C4/C5) ------------------------------------------------
 
-
-def batch_specs(name, nstreams=0):
+def batch_specs(name, nstreams=0, eblocks=0):
+    """[(bits, channels, eblocks)] of a batch config."""
     if name == "C4":
         n = nstreams or 1024
-        return [((4, 6, 8)[i % 3], 1 + ((i // 3) & 1), 16384) for i in range(n)]
+        return [((4, 6, 8)[i % 3], 1 + ((i // 3) & 1), eblocks or 16384) for i in range(n)]
     if name == "C5":
-        return [(8, 2, 65536)] * (nstreams or 1024)
-    return [(8, 2, 65536)] * (nstreams or 128)
+        return [(8, 2, eblocks or 65536)] * (nstreams or 1024)
+    return [(8, 2, eblocks or 65536)] * (nstreams or 128)
 
 
 def shard_range(n, rank, world):
@@ -208,87 +293,141 @@ def shard_range(n, rank, world):
     return rank * n // world, (rank + 1) * n // world
 
 
-def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1):
-    """Decode a batch config (bjxa_hip_batch_*: all streams per launch)
-    `steps` times after `warmup` untimed steps.  With world > 1 this rank
-    takes a contiguous share of the streams (seeded by global index, so the
-    job is the same at every N) and the timed region is bracketed by
-    barriers."""
-    import torch
-    import torch.distributed as dist
-    import bjxa_amd
+def batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream=-1):
+    """Seeded XA of streams lo..hi-1 of a batch job (seed = 1000 + global
+    index, so the job is the same at every N); `bad_stream` gets a gain-5
+    profile in its middle eblock (first-error collective test)."""
     from bjxa_amd import synth
-    specs = batch_specs(name, nstreams)
-    lo, hi = shard_range(len(specs), rank, world)
-    xas, srcs, dsts, streams = [], [], [], []
-    samples = alg = 0
+    specs = batch_specs(name, nstreams, eblocks)
+    out = []
     for i in range(lo, hi):
         bits, ch, eb = specs[i]
         xa = synth.stream(eb, bits, ch, "A", seed=1000 + i)
+        if i == bad_stream:
+            xa[(eb // 2) * ch * (bits * 4 + 1)] = 0x57
+        out.append((i, bits, ch, eb, xa))
+    return out
+
+
+def oracle_batch(inputs, threads):
+    """Oracle decode of a list of streams on `threads` host threads (one
+    decoder per thread, streams round-robin); returns {index: pcm} and the
+    seconds it took."""
+    import oracle
+    res = {}
+
+    def work(k):
+        for j in range(k, len(inputs), threads):
+            i, bits, ch, eb, xa = inputs[j]
+            res[i] = oracle.decode(xa, eb, bits, ch)
+    t = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return res, time.perf_counter() - t
+
+
+def cpu_batch_baseline(name, inputs):
+    """C4/C5 CPU baseline: the oracle on all usable host cores."""
+    threads, online = cpu_threads()
+    samples = sum(eb * 32 * ch for _, _, ch, eb, _ in inputs)
+    oracle_batch(inputs, threads)                       # discarded first pass
+    times = [oracle_batch(inputs, threads)[1] for _ in range(CPU_PASSES)]
+    med = float(np.median(times))
+    return {"value": round(samples / med / 1e6, 1), "unit": "MSamples/s", "cores": threads,
+            "kind": "port",
+            "sample": "all %d streams of %s (%d samples), oracle/xa_oracle.c single-pass decode, "
+                      "one decoder per thread on %d threads, streams round-robin, median of %d "
+                      "passes after a discarded first; host: %s, %s CPUs online"
+                      % (len(inputs), name, samples, threads, CPU_PASSES, host_cpu(), online)}
+
+
+def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, eblocks=0,
+              cpu_leg=False, bad_stream=-1):
+    """Decode (this rank's share of) a batch config with bjxa_hip_batch_* --
+    all streams per launch -- `steps` times after `warmup` untimed steps,
+    then time EV_SAMPLES more launches with events.  Returns this rank's
+    measurements incl. per-stream checksums and first failing stream."""
+    import torch
+    import torch.distributed as dist
+    import bjxa_amd
+    specs = batch_specs(name, nstreams, eblocks)
+    lo, hi = shard_range(len(specs), rank, world)
+    inputs = batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream)
+    srcs, dsts, streams = [], [], []
+    samples = alg = 0
+    for i, bits, ch, eb, xa in inputs:
         s = torch.from_numpy(xa).to(dev)
         d = torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
-        xas.append(xa)
         srcs.append(s)
         dsts.append(d)
         streams.append({"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
                         "bits": bits, "channels": ch})
         samples += eb * 32 * ch
         alg += xa.nbytes + eb * 64 * ch
-    specs = specs[lo:hi]
-    status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
+    n = len(inputs)
+    status = torch.zeros(max(n, 1) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
-    hip = hip_runtime()
-    evs = []
-    for _ in range(steps + warmup):
-        a, b = ctypes.c_void_p(), ctypes.c_void_p()
-        hip.hipEventCreate(ctypes.byref(a))
-        hip.hipEventCreate(ctypes.byref(b))
-        evs.append((a.value, b.value))
-    with bjxa_amd.Batch(streams, stream=sh) as batch:
-        for i in range(warmup):
-            batch.decode(status.data_ptr(), sh, evs[i])
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for i in range(warmup, warmup + steps):
-            batch.decode(status.data_ptr(), sh,
-                         evs[i] if (i - warmup) % EV_EVERY == 0 else (None, None))
-        torch.cuda.synchronize(dev)
-        elapsed = time.perf_counter() - t0
-        if world > 1:
-            dist.barrier()
-        dt = elapsed / steps
-    spec = []
-    for i in range(warmup, warmup + steps):
-        if (i - warmup) % EV_EVERY:
-            continue
-        a, b = evs[i]
-        f = ctypes.c_float()
-        hip.hipEventElapsedTime(ctypes.byref(f), a, b)
-        spec.append(f.value)
-    for a, b in evs:
-        hip.hipEventDestroy(a)
-        hip.hipEventDestroy(b)
-    spec_ms = float(np.mean(spec))
-    st = status.cpu().numpy().view(np.uint32).reshape(len(specs), -1)
-    ok = None
+    elapsed, spec = 0.0, [0.0]
+    if n:
+        with bjxa_amd.Batch(streams, stream=sh) as batch:
+            for _ in range(warmup):
+                batch.decode(status.data_ptr(), sh)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                batch.decode(status.data_ptr(), sh)
+            torch.cuda.synchronize(dev)
+            elapsed = time.perf_counter() - t0
+            if world > 1:
+                dist.barrier()
+            evs = EventPairs(max(EV_SAMPLES, steps))
+            for ev in evs.ev:
+                batch.decode(status.data_ptr(), sh, ev)
+            spec = evs.ms()
+            evs.close()
+    elif world > 1:
+        dist.barrier()
+        dist.barrier()
+    spec_ms = float(np.median(spec))
+    st = status.cpu().numpy().view(np.uint32).reshape(max(n, 1), -1)[:n]
+    # a failed stream counts only the PCM before its failing eblock
+    valid = [eb * 32 * ch if int(w[0]) == NO_ERROR else int(w[0]) // ch * 32 * ch
+             for (_, _, ch, eb, _), w in zip(inputs, st)]
+    sums = [pcm_checksum_torch(d, v) for d, v in zip(dsts, valid)]
+    first_err = min([i for (i, *_), w in zip(inputs, st) if int(w[0]) != NO_ERROR],
+                    default=FIRST_ERR_NONE)
+    ok, ref_sums = None, None
     if verify:
-        import oracle
-        ok = True
-        for (bits, ch, eb), xa, d in zip(specs, xas, dsts):
-            ref, _, _, _ = oracle.decode(xa, eb, bits, ch)
-            if not np.array_equal(d.cpu().numpy().view(np.int16), ref):
+        threads, _ = cpu_threads()
+        refs, _ = oracle_batch(inputs, max(1, threads // world))
+        ok, ref_sums = True, []
+        for (i, bits, ch, eb, xa), d, w in zip(inputs, dsts, st):
+            pcm, _, done, _ = refs[i]
+            ref_sums.append(pcm_checksum_np(pcm[:done * 32 * ch]))
+            if int(w[0]) != NO_ERROR:       # compare up to the failing eblock
+                m = done * 32 * ch
+                ok = ok and bool(np.array_equal(d.cpu().numpy().view(np.int16)[:m], pcm[:m]))
+            elif not np.array_equal(d.cpu().numpy().view(np.int16), pcm):
                 ok = False
-                break
-    return {"workload": BATCHES.get(name, name), "streams": len(specs),
+        del refs
+    cpu = cpu_batch_baseline(name, inputs) if cpu_leg else None
+    return {"workload": BATCHES.get(name, name), "streams": n, "shard": [lo, hi],
             "samples": samples, "elapsed": elapsed,
-            "value": round(samples / dt / 1e6, 1), "unit": "MSamples/s",
-            "ms_per_step": round(dt * 1e3, 4), "spec_ms": round(spec_ms, 4),
-            "frac": round(alg / (spec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "alg_bytes": alg, "repaired": int(st[:, 3].sum()), "tail": int(st[:, 4].sum()),
-            "chunks": int(st[:, 5].sum()), "bit_exact": ok}
+            "value": round(samples * steps / elapsed / 1e6, 1) if elapsed else 0.0,
+            "unit": "MSamples/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "spec_ms": round(spec_ms, 4), "spec_samples": len(spec),
+            "frac": round(alg / (spec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if spec_ms else 0.0,
+            "alg_bytes": alg, "repaired": int(st[:, 3].sum()) if n else 0,
+            "tail": int(st[:, 4].sum()) if n else 0, "chunks": int(st[:, 5].sum()) if n else 0,
+            "bit_exact": ok, "checksums": sums, "ref_checksums": ref_sums,
+            "first_error": first_err, "cpu_baseline": cpu}
 
 
 def run_encode(steps, warmup, dev, verify):
@@ -307,15 +446,22 @@ def run_encode(steps, warmup, dev, verify):
     for _ in range(warmup):
         bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
     torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    e0.record()
     for _ in range(steps):
         bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
-    e1.record()
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
-    ms = e0.elapsed_time(e1) / steps
+    # per-launch kernel time: events around each of EV_SAMPLES launches
+    # (encode is one kernel, so torch's events on the same stream suffice)
+    ms = []
+    for _ in range(max(EV_SAMPLES, steps)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
+        e1.record()
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    med = float(np.median(ms))
     ok = None
     if verify:
         import oracle
@@ -323,8 +469,9 @@ def run_encode(steps, warmup, dev, verify):
     alg = pcm.nbytes + nxa
     return {"workload": "encode, C3-shaped: 320M int16 samples (8-bit stereo) -> XA",
             "value": round(frames * ch / dt / 1e6, 1), "unit": "MSamples/s",
-            "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(ms, 4),
-            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
+            "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(med, 4),
+            "kernel_samples": len(ms),
+            "frac": round(alg / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
             "byte_exact": ok}
 
 
@@ -342,22 +489,35 @@ def pmc_traffic(workload, mix):
     return None, None
 
 
-def main():
+# ---- entry ------------------------------------------------------------------
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS) + ["C5"],
-                    help="C3/C2: one stream per rank (weak scaling); C5: 1024 "
-                         "streams split over the ranks (strong scaling)")
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS) + ["C5"],
+                    help="default: C3 at N=1 (one stream per rank), C5 at N>1 (the "
+                         "1024-stream job split over the ranks)")
     ap.add_argument("--mix", default="A", choices=["A", "F", "W", "Z"])
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--warm-blocks", type=int, default=-1)
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--streams", type=int, default=0, help="C5 streams (default 1024)")
+    ap.add_argument("--eblocks", type=int, default=0, help="C5 eblocks per stream (65,536)")
+    ap.add_argument("--bad-stream", type=int, default=-1,
+                    help="C5: give this stream a gain-5 profile (first-error collective)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true",
-                    help="skip the C2/C4/C5g lines at N=1")
-    args = ap.parse_args()
+                    help="skip the other_configs lines")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the parent never touches the GPU: it only starts the ranks
+        return launch_ranks(args.gpus)
 
     import torch
     import torch.distributed as dist
@@ -365,16 +525,42 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("BJXA_BENCH_BACKEND", "nccl")
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        return 2
+    if backend == "gloo":
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        return main_c5_cpu(args, dev, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    workload = args.workload or ("C3" if world == 1 else "C5")
+    try:
+        if workload == "C5":
+            return main_c5(args, dev, world, rank)
+        return main_stream(args, workload, dev, world, rank)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
 
-    if args.workload == "C5":
-        return main_c5(args, dev, world, rank)
 
+def other_stream_line(o, steps, world=1):
+    return {"workload": o["desc"] + (" per rank" if world > 1 else ""),
+            "value": round(job_value(o["samples"], world, steps, o["elapsed"]), 1),
+            "unit": "MSamples/s", "ms_per_step": round(o["elapsed"] / steps * 1e3, 4),
+            "spec_ms": round(o["spec_ms"], 4), "spec_samples": o["spec_samples"],
+            "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "chunk": int(o["status"][6]), "bit_exact": o["ok"], "cpu_baseline": o["cpu"]}
+
+
+def main_stream(args, workload, dev, world, rank):
+    """C3 (or C2): one stream per rank, weak scaling."""
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu
-    r = run_workload(args.workload, args, dev, world, rank, not args.no_verify, cpu_leg)
+    r = run_workload(workload, args, dev, world, rank, not args.no_verify, cpu_leg)
     elapsed, ok = r["elapsed"], r["ok"]
     if world > 1:
         elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
@@ -382,19 +568,18 @@ def main():
     other = {}
     if world == 1 and not args.no_other:
         for name in sorted(WORKLOADS):
-            if name == args.workload:
+            if name == workload:
                 continue
-            o = run_workload(name, args, dev, 1, rank, not args.no_verify, False)
-            other[name] = {
-                "workload": o["desc"], "value": round(job_value(o["samples"], 1, args.steps,
-                                                                o["elapsed"]), 1),
-                "unit": "MSamples/s", "ms_per_step": round(o["elapsed"] / args.steps * 1e3, 4),
-                "spec_ms": round(o["spec_ms"], 4),
-                "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "chunk": int(o["status"][6]), "bit_exact": o["ok"]}
+            o = run_workload(name, args, dev, 1, rank, not args.no_verify, cpu_leg)
+            other[name] = other_stream_line(o, args.steps)
             ok = ok if o["ok"] in (None, True) else False
         for name in sorted(BATCHES):
-            o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify)
+            o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify,
+                          cpu_leg=cpu_leg and name in ("C4", "C5"))
+            for k in ("checksums", "ref_checksums", "shard"):
+                o.pop(k)
+            if o["first_error"] == FIRST_ERR_NONE:
+                o["first_error"] = None
             other[name] = o
             ok = ok if o["bit_exact"] in (None, True) else False
         o = run_encode(args.steps, args.warmup, dev, not args.no_verify)
@@ -404,9 +589,9 @@ def main():
     st = r["status"]
     achieved = r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9
     read_gbs = r["xa_bytes"] / (r["spec_ms"] * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.workload, args.mix)
+    traffic, traffic_src = pmc_traffic(workload, args.mix)
     line = {
-        "metric": "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs CPU",
+        "metric": METRIC,
         "value": round(job_value(r["samples"], world, args.steps, elapsed), 1),
         "unit": "MSamples/s",
         "n_gpus": world,
@@ -418,7 +603,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int32+f32",
         "data": "synthetic (seeded XA stream, profile mix %s, uniform codes)" % args.mix,
-        "config": {"workload": r["desc"] + " per rank", "workload_id": args.workload,
+        "config": {"workload": r["desc"] + " per rank", "workload_id": workload,
                    "bits": r["bits"], "channels": r["ch"],
                    "eblocks_per_rank": r["eb"], "samples_per_rank": r["samples"],
                    "profile_mix": args.mix, "parallelism": "independent streams, 1 per GPU",
@@ -430,7 +615,10 @@ def main():
                      "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": traffic_src,
                      "read_only_achieved": round(read_gbs, 1),
                      "read_only_frac": round(read_gbs / HBM_PEAK_GBS, 4),
-                     "launch_ms": round(r["spec_ms"], 4)},
+                     "launch_ms": round(r["spec_ms"], 4),
+                     "launch_ms_stat": "median of %d launches" % r["spec_samples"],
+                     "step_frac": round(r["alg_bytes"] / (elapsed / args.steps) / 1e9 /
+                                        HBM_PEAK_GBS / world, 4)},
         "cpu_baseline": r["cpu"],
         "bit_exact": ok,
         "repaired_chunks": int(st[3]), "tail_repairs": int(st[4]), "chunks": int(st[5]),
@@ -439,37 +627,188 @@ def main():
         line["other_configs"] = other
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
     return 0 if ok in (None, True) else 1
+
+
+def c5_control_plane(r, dev, world, nstreams):
+    """SURVEY.md §5 collectives of the batched job: AllReduce(sum) of the
+    counters, AllReduce(min) of the first failing stream, AllGather of the
+    per-stream PCM checksums (padded shares) -- GPU's and oracle's -- which
+    rank 0 compares.  Returns the job-wide view."""
+    import torch
+    import torch.distributed as dist
+    cnt = torch.tensor([r["samples"], r["alg_bytes"], r["repaired"], r["tail"], r["chunks"],
+                        r["streams"]], dtype=torch.int64, device=dev)
+    fe = torch.tensor([r["first_error"]], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        dist.all_reduce(fe, op=dist.ReduceOp.MIN)
+    width = (nstreams + world - 1) // world
+    have_ref = r["ref_checksums"] is not None
+
+    def gather(vals):
+        t = torch.zeros(width + 1, dtype=torch.int64, device=dev)
+        t[0] = len(vals)
+        if vals:
+            t[1:1 + len(vals)] = torch.tensor(vals, dtype=torch.int64)
+        if world == 1:
+            return [t]
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        return parts
+
+    def flat(parts):
+        return [int(v) for p in parts for v in p[1:1 + int(p[0])].tolist()]
+    sums = flat(gather(r["checksums"]))
+    refs = flat(gather(r["ref_checksums"] or [])) if have_ref else None
+    shards = gather([r["shard"][0], r["shard"][1]])
+    c = [int(v) for v in cnt.tolist()]
+    return {"samples": c[0], "alg_bytes": c[1], "repaired": c[2], "tail": c[3],
+            "chunks": c[4], "streams": c[5], "first_error": int(fe.item()),
+            "checksums": sums, "ref_checksums": refs,
+            "shards": [[int(p[1]), int(p[2])] for p in shards]}
+
+
+def checksum_report(job):
+    """Digest of the gathered checksum vector and rank 0's comparison."""
+    import hashlib
+    h = hashlib.sha1(np.array(job["checksums"], dtype=np.int64).tobytes()).hexdigest()
+    match = None
+    if job["ref_checksums"] is not None:
+        match = job["checksums"] == job["ref_checksums"]
+    return h, match
 
 
 def main_c5(args, dev, world, rank):
     """C5: the fixed job of 1024 8-bit stereo streams (65,536 eblocks each)
     split over the ranks -- strong scaling, no data-path collective."""
-    import torch.distributed as dist
-    r = run_batch("C5", args.steps, args.warmup, dev, not args.no_verify, 0, rank, world)
+    nstreams = args.streams or 1024
+    r = run_batch("C5", args.steps, args.warmup, dev, not args.no_verify, nstreams, rank,
+                  world, args.eblocks, bad_stream=args.bad_stream)
     elapsed, ok = r["elapsed"], r["bit_exact"]
     if world > 1:
         elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
-    total = 1024 * 65536 * 64
+    job = c5_control_plane(r, dev, world, nstreams)
+    digest, match = checksum_report(job)
+    if match is False:
+        ok = False
+    # per-rank kernel times for the report
+    import torch
+    import torch.distributed as dist
+    lm = torch.tensor([r["spec_ms"], r["frac"]], dtype=torch.float64, device=dev)
+    parts = [torch.zeros_like(lm) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(parts, lm)
+    else:
+        parts = [lm]
+    per_rank = [[round(float(p[0]), 4), round(float(p[1]), 4)] for p in parts]
+
+    other = {}
+    if not args.no_other and world > 1:
+        o = run_workload("C3", args, dev, world, rank, not args.no_verify, False)
+        el, ok3 = reduce_over_ranks(o["elapsed"], o["ok"], dev)
+        o["elapsed"] = el
+        o["ok"] = ok3
+        other["C3_weak"] = other_stream_line(o, args.steps, world)
+        ok = ok if ok3 in (None, True) else False
+
+    spec_ms = r["spec_ms"]
     line = {
-        "metric": "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs CPU",
-        "value": round(total * args.steps / elapsed / 1e6, 1), "unit": "MSamples/s",
+        "metric": METRIC,
+        "value": round(job["samples"] * args.steps / elapsed / 1e6, 1), "unit": "MSamples/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int32+f32",
         "data": "synthetic (seeded XA streams, profile mix A, uniform codes)",
-        "config": {"workload": BATCHES["C5"], "workload_id": "C5",
-                   "streams_per_rank": r["streams"],
-                   "parallelism": "stream shards, one batched launch per GPU"},
+        "config": {"workload": BATCHES["C5"] if not (args.streams or args.eblocks) else
+                   "C5-shaped: %d 8-bit stereo streams of %d eblocks, a contiguous share "
+                   "per rank" % (nstreams, batch_specs("C5", nstreams, args.eblocks)[0][2]),
+                   "workload_id": "C5", "streams": job["streams"],
+                   "streams_per_rank": [hi - lo for lo, hi in job["shards"]],
+                   "parallelism": "stream shards, one batched launch per GPU, RCCL control "
+                                  "plane only"},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec_batch (rank 0)",
-                     "achieved": round(r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9, 1),
+                     "achieved": round(r["alg_bytes"] / (spec_ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["frac"],
                      "traffic": None, "alg_bytes_per_launch": r["alg_bytes"],
-                     "launch_ms": r["spec_ms"]},
+                     "launch_ms": spec_ms,
+                     "launch_ms_stat": "median of %d launches" % r["spec_samples"],
+                     "per_rank_launch_ms_frac": per_rank},
         "cpu_baseline": None, "bit_exact": ok,
+        "control_plane": {"shards": job["shards"], "samples": job["samples"],
+                          "repaired_chunks": job["repaired"], "tail_repairs": job["tail"],
+                          "first_error_stream": None if job["first_error"] >= FIRST_ERR_NONE
+                          else job["first_error"],
+                          "checksums_sha1": digest, "checksums_match_oracle": match},
     }
+    if other:
+        line["other_configs"] = other
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0 if ok in (None, True) else 1
+
+
+def main_c5_cpu(args, dev, world, rank):
+    """CPU rehearsal of the N > 1 path (gloo): this rank's share of a small
+    C5-shaped job decoded with the library's host API (its CPU core), then
+    the same control plane as main_c5."""
+    import torch.distributed as dist
+    import bjxa_amd
+    nstreams = args.streams or 16
+    eblocks = args.eblocks or 1000
+    specs = batch_specs("C5", nstreams, eblocks)
+    lo, hi = shard_range(len(specs), rank, world)
+    inputs = batch_inputs("C5", nstreams, eblocks, lo, hi, args.bad_stream)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    first_err, pcms = FIRST_ERR_NONE, {}
+    with bjxa_amd.offload(None):
+        for _ in range(args.steps):
+            for i, bits, ch, eb, xa in inputs:
+                pcm = np.zeros(eb * 32 * ch, np.int16)
+                with bjxa_amd.Decoder() as d:
+                    d.parse_header(bjxa_amd.xa_header(xa.size, eb * 32, 44100, bits, ch))
+                    try:
+                        d.decode(pcm, xa)
+                        pcms[i] = pcm
+                    except bjxa_amd.BjxaError:
+                        # the PCM before the failing eblock (none past it)
+                        first_err = min(first_err, i)
+                        bad = next(b for b in range(eb) if any(
+                            xa[(b * ch + c) * (bits * 4 + 1)] >= 0x50 for c in range(ch)))
+                        pcms[i] = pcm[:bad * 32 * ch]
+    elapsed = time.perf_counter() - t0
+    sums = [pcm_checksum_np(pcms[i]) for i, *_ in inputs]
+    ok, refs = None, None
+    if not args.no_verify:
+        ref, _ = oracle_batch(inputs, 1)
+        refs = [pcm_checksum_np(ref[i][0][:ref[i][2] * 32 * ch]) for i, bits, ch, eb, xa in inputs]
+        ok = sums == refs
+    if world > 1:
+        elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
+    samples = sum(eb * 32 * ch for _, _, ch, eb, _ in inputs)
+    r = {"samples": samples, "alg_bytes": 0, "repaired": 0, "tail": 0, "chunks": 0,
+         "streams": len(inputs), "first_error": first_err, "checksums": sums,
+         "ref_checksums": refs, "shard": [lo, hi]}
+    job = c5_control_plane(r, dev, world, nstreams)
+    digest, match = checksum_report(job)
+    if match is False:
+        ok = False
+    line = {"metric": METRIC, "value": round(job["samples"] * args.steps / elapsed / 1e6, 1),
+            "unit": "MSamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "int32", "data": "synthetic (seeded XA streams, profile mix A)",
+            "device": "cpu (gloo rehearsal of the RCCL path; library host API on its CPU core)",
+            "config": {"workload": "C5-shaped: %d streams of %d eblocks" % (nstreams, eblocks),
+                       "workload_id": "C5", "streams": job["streams"],
+                       "streams_per_rank": [b - a for a, b in job["shards"]]},
+            "bit_exact": ok,
+            "control_plane": {"shards": job["shards"], "samples": job["samples"],
+                              "first_error_stream": None if job["first_error"] >= FIRST_ERR_NONE
+                              else job["first_error"],
+                              "checksums_sha1": digest, "checksums_match_oracle": match}}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

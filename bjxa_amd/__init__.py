@@ -11,8 +11,10 @@ C-ABI for the tests and the benchmark:
 * :func:`decode_device` / :func:`encode_device` expose the device-resident
   extension (include/bjxa_hip.h) on raw device pointers.
 
-There is no CPU compute path: decode/encode need the GPU kernels and fail
-with ENODEV without a GPU.  A missing library raises immediately.
+Host-buffer calls below the offload threshold (and every call on a host
+without a GPU) run on the library's CPU core (csrc/xa_cpu.c); the
+device-resident entry points always run the HIP kernels and fail with
+ENODEV without a GPU.  A missing library raises immediately.
 
 Processes that also use PyTorch must import torch before calling
 :func:`lib` so both share one HIP runtime.
@@ -102,6 +104,8 @@ _SIGS = {
     "bjxa_hip_decode_files": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_uint32]),
     # LIBBJXA_HIP_0.2
     "bjxa_hip_parse_headers_async": (ctypes.c_int, [_P, _SZ, ctypes.c_uint32, _P, _P]),
+    # LIBBJXA_HIP_0.3
+    "bjxa_hip_offload_threshold": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int64]),
 }
 REFERENCE_SYMBOLS = {  # src/libbjxa.map:16-47
     "LIBBJXA_0.1": ["bjxa_decode", "bjxa_decode_format", "bjxa_decoder", "bjxa_dump_pcm",
@@ -116,7 +120,8 @@ EXTENSION_SYMBOLS = {"LIBBJXA_HIP_0.1": ["bjxa_hip_batch_decode_async", "bjxa_hi
                                          "bjxa_hip_decode_files",
                                          "bjxa_hip_decode_workspace", "bjxa_hip_encode_async",
                                          "bjxa_hip_version", "bjxa_hip_workspace_init"],
-                     "LIBBJXA_HIP_0.2": ["bjxa_hip_parse_headers_async"]}
+                     "LIBBJXA_HIP_0.2": ["bjxa_hip_parse_headers_async"],
+                     "LIBBJXA_HIP_0.3": ["bjxa_hip_offload_threshold"]}
 
 
 def lib():
@@ -401,6 +406,33 @@ def parse_headers_device(d_src, stride, n, d_out, stream=0):
 def encode_device(d_pcm, frames, bits, channels, d_xa, stream=0):
     _check(lib().bjxa_hip_encode_async(d_pcm, frames, bits, channels, d_xa, stream),
            "bjxa_hip_encode_async")
+
+
+OFFLOAD_DECODE, OFFLOAD_ENCODE = 0, 1
+
+
+def offload_threshold(direction, cblocks=-1):
+    """bjxa_hip_offload_threshold: set (cblocks >= 0) or query the number
+    of channel blocks from which bjxa_decode/bjxa_encode run on the GPU;
+    returns the previous value."""
+    return _check(lib().bjxa_hip_offload_threshold(direction, cblocks),
+                  "bjxa_hip_offload_threshold")
+
+
+class offload:
+    """Context manager routing host-API calls: offload(0) sends every call
+    to the GPU, offload(None) none (CPU core only)."""
+
+    def __init__(self, cblocks):
+        self.v = (1 << 63) - 1 if cblocks is None else cblocks
+
+    def __enter__(self):
+        self.old = [offload_threshold(d, self.v) for d in (OFFLOAD_DECODE, OFFLOAD_ENCODE)]
+        return self
+
+    def __exit__(self, *a):
+        for d, v in zip((OFFLOAD_DECODE, OFFLOAD_ENCODE), self.old):
+            offload_threshold(d, v)
 
 
 def version():

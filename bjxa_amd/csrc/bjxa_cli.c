@@ -15,12 +15,18 @@
  * files that cannot be opened, and "<libbjxa call>: <strerror>" for codec
  * errors; the exit status is then 1.
  *
- * Call shape: one bjxa_decode()/bjxa_encode() per stream -- the reference's
- * BJXA_SINGLE_PASS build (src/bjxa_decode.c:56-100, src/bjxa_encode.c:
- * 62-110) and the shape the GPU path is built for.  BJXA_CLI_BLOCKS=1 in
- * the environment selects the reference's default one-block-per-call loop
- * (src/bjxa_decode.c:102-155) instead; the output is the same.
+ * Call shape: by default the whole stream is read and handed to one
+ * bjxa_decode()/bjxa_encode() call -- the reference's BJXA_SINGLE_PASS shape
+ * (src/bjxa_decode.c:56-100, src/bjxa_encode.c:62-110), which lets a large
+ * stream run on the GPU -- but the output on failure is that of the
+ * reference's default one-block-per-call loop (src/bjxa_decode.c:102-155,
+ * src/bjxa_encode.c:108-176): a stream cut short yields every whole block
+ * that was read, then "fread: End of file"; a block whose gain nibble is
+ * >= 5 yields the PCM of every block before it, then "bjxa_decode:
+ * Protocol error".  BJXA_CLI_BLOCKS=1 selects the one-block-per-call loop
+ * itself; both shapes write the same bytes.
  */
+#include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -78,16 +84,35 @@ redirect(int argc, char *const *argv)
 	return (0);
 }
 
+static void
+read_error(FILE *in)
+{
+	if (feof(in))
+		fprintf(stderr, "fread: End of file\n");
+	else
+		perror("fread");
+}
+
 static int
 read_exact(void *buf, size_t len, FILE *in)
 {
 	if (len == 0 || fread(buf, len, 1, in) == 1)
 		return (0);
-	if (feof(in))
-		fprintf(stderr, "fread: End of file\n");
-	else
-		perror("fread");
+	read_error(in);
 	return (-1);
+}
+
+/* first eblock of `n` holding a channel block whose gain nibble is >= 5
+ * (the reference's EPROTO, src/libbjxa.c:547-550), or n */
+static uint32_t
+first_bad_block(const uint8_t *xa, uint32_t n, const bjxa_format_t *fmt)
+{
+	const unsigned bsz = fmt->block_size_xa / fmt->channels;
+	for (uint32_t b = 0; b < n; b++)
+		for (unsigned c = 0; c < fmt->channels; c++)
+			if (xa[(size_t)b * fmt->block_size_xa + c * bsz] >= 0x50)
+				return (b);
+	return (n);
 }
 
 static int
@@ -97,26 +122,55 @@ block_calls(void)
 	return (e != NULL && *e != '\0' && strcmp(e, "0") != 0);
 }
 
-/* one call over the whole stream */
+/*
+ * One call over the whole stream, with the per-block loop's output on
+ * failure: the PCM of the whole blocks that were read (up to a bad block)
+ * is written before the error is reported.
+ */
 static int
 decode_stream(bjxa_decoder_t *dec, const bjxa_format_t *fmt, FILE *in,
     FILE *out)
 {
-	const size_t xa_len = (size_t)fmt->block_size_xa * fmt->blocks;
-	void *xa = malloc(xa_len + 1), *pcm = malloc((size_t)fmt->data_len_pcm + 1);
-	int rc = -1;
+	/* room for one whole block even when the stream is shorter, as the
+	 * per-block loop passes (a sub-block single pass is ENOBUFS) */
+	const size_t pcm_len = fmt->data_len_pcm > fmt->block_size_pcm ?
+	    fmt->data_len_pcm : fmt->block_size_pcm;
+	uint8_t *xa = malloc((size_t)fmt->block_size_xa * fmt->blocks + 1);
+	void *pcm = malloc(pcm_len);
+	uint32_t got, good;
+	size_t bytes;
+	int rc = -1, bad = 0;
 
-	if (xa == NULL || pcm == NULL)
+	if (xa == NULL || pcm == NULL) {
 		perror("malloc");
-	else if (read_exact(xa, xa_len, in) == 0) {
-		if (bjxa_decode(dec, pcm, fmt->data_len_pcm, xa, xa_len) !=
-		    (int)fmt->blocks)
-			perror("bjxa_decode");
-		else if (bjxa_fwrite_pcm(pcm, fmt->data_len_pcm, out) < 0)
-			perror("bjxa_fwrite_pcm");
-		else
-			rc = 0;
+		goto done;
 	}
+	got = (uint32_t)fread(xa, fmt->block_size_xa, fmt->blocks, in);
+	good = got;
+	if (got > 0 && bjxa_decode(dec, pcm, pcm_len, xa,
+	    (size_t)got * fmt->block_size_xa) != (int)got) {
+		const int e = errno;
+		good = first_bad_block(xa, got, fmt);
+		bad = 1;
+		errno = e;
+	}
+	bytes = (size_t)good * fmt->block_size_pcm;
+	if (bytes > fmt->data_len_pcm)
+		bytes = fmt->data_len_pcm;
+	if (bad) {
+		const int e = errno;
+		if (bytes > 0)
+			(void)bjxa_fwrite_pcm(pcm, bytes, out);
+		errno = e;
+		perror("bjxa_decode");
+	} else if (bytes > 0 && bjxa_fwrite_pcm(pcm, bytes, out) < 0) {
+		perror("bjxa_fwrite_pcm");
+	} else if (got < fmt->blocks) {
+		read_error(in);
+	} else {
+		rc = 0;
+	}
+done:
 	free(xa);
 	free(pcm);
 	return (rc);
@@ -182,25 +236,38 @@ cmd_decode(FILE *in, FILE *out)
 	return (rc);
 }
 
+/* one call over the whole stream; on a short read, the XA of the blocks
+ * whose PCM was complete is written before the error (as the per-block
+ * loop does) */
 static int
 encode_stream(bjxa_encoder_t *enc, const bjxa_format_t *fmt, FILE *in,
     FILE *out)
 {
 	const size_t xa_len = (size_t)fmt->block_size_xa * fmt->blocks;
-	void *xa = malloc(xa_len + 1), *pcm = malloc((size_t)fmt->data_len_pcm + 1);
+	const size_t pcm_len = fmt->data_len_pcm > fmt->block_size_pcm ?
+	    fmt->data_len_pcm : fmt->block_size_pcm;
+	void *xa = malloc(xa_len + 1), *pcm = malloc(pcm_len);
+	size_t got;
+	uint32_t n;
 	int rc = -1;
 
-	if (xa == NULL || pcm == NULL)
+	if (xa == NULL || pcm == NULL) {
 		perror("malloc");
-	else if (read_exact(pcm, fmt->data_len_pcm, in) == 0) {
-		if (bjxa_encode(enc, xa, xa_len, pcm, fmt->data_len_pcm) !=
-		    (int)fmt->blocks)
-			perror("bjxa_encode");
-		else if (xa_len > 0 && fwrite(xa, xa_len, 1, out) != 1)
-			perror("fwrite");
-		else
-			rc = 0;
+		goto done;
 	}
+	got = fread(pcm, 1, fmt->data_len_pcm, in);
+	n = got == fmt->data_len_pcm ? fmt->blocks :
+	    (uint32_t)(got / fmt->block_size_pcm);
+	if (n > 0 && bjxa_encode(enc, xa, xa_len, pcm, got == fmt->data_len_pcm ?
+	    pcm_len : (size_t)n * fmt->block_size_pcm) != (int)n)
+		perror("bjxa_encode");
+	else if (n > 0 && fwrite(xa, (size_t)n * fmt->block_size_xa, 1, out) != 1)
+		perror("fwrite");
+	else if (n < fmt->blocks)
+		read_error(in);
+	else
+		rc = 0;
+done:
 	free(xa);
 	free(pcm);
 	return (rc);

@@ -2,7 +2,9 @@
  * libbjxa.c -- host side of the MI355X libbjxa: codec objects, XA header
  * and RIFF/WAVE framing, the errno contract, and per-call bookkeeping.
  * The block arithmetic of bjxa_decode()/bjxa_encode() runs on the GPU
- * (xa_decode.hip / xa_encode.hip via xa_gpu.hip); there is no CPU path.
+ * (xa_decode.hip / xa_encode.hip via xa_gpu.hip) for calls of at least
+ * the offload threshold, and on the calling thread's core (xa_cpu.c) for
+ * smaller calls and on hosts without a GPU ("Routing").
  *
  * Each entry point restates the behaviour of the reference routine cited
  * next to it (paths relative to the reference checkout), including its
@@ -13,6 +15,7 @@
 
 #include <assert.h>
 #include <errno.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -97,6 +100,64 @@ read_all(void *buf, size_t n, FILE *file)
 		return (-1);
 	}
 	return (0);
+}
+
+/* ---- CPU / GPU routing (LIBBJXA_HIP_0.3) ------------------------------- */
+
+/*
+ * A call of at least offload_min[dir] channel blocks runs on the GPU,
+ * a smaller one on the calling core.  Defaults are the measured crossover
+ * points of tools/call_latency.py; BJXA_OFFLOAD_DECODE and
+ * BJXA_OFFLOAD_ENCODE (channel blocks) override them at load time, and
+ * bjxa_hip_offload_threshold() at run time.
+ */
+#define OFFLOAD_DECODE_DEFAULT	2048u
+#define OFFLOAD_ENCODE_DEFAULT	8192u
+
+static uint64_t offload_min[2];
+static pthread_once_t offload_once = PTHREAD_ONCE_INIT;
+
+static void
+offload_init(void)
+{
+	static const char *const env[2] = { "BJXA_OFFLOAD_DECODE",
+	    "BJXA_OFFLOAD_ENCODE" };
+	const uint64_t dflt[2] = { OFFLOAD_DECODE_DEFAULT,
+	    OFFLOAD_ENCODE_DEFAULT };
+
+	for (int d = 0; d < 2; d++) {
+		const char *v = getenv(env[d]);
+		char *end;
+		unsigned long long n = 0;
+		if (v != NULL && *v != '\0')
+			n = strtoull(v, &end, 10);
+		__atomic_store_n(&offload_min[d], (v != NULL && *v != '\0' &&
+		    *end == '\0') ? (uint64_t)n : dflt[d], __ATOMIC_RELAXED);
+	}
+}
+
+static int
+on_gpu(int dir, uint64_t cblocks)
+{
+	(void)pthread_once(&offload_once, offload_init);
+	return cblocks >= __atomic_load_n(&offload_min[dir], __ATOMIC_RELAXED) &&
+	    bjxa__gpu_present();
+}
+
+int64_t
+bjxa_hip_offload_threshold(int direction, int64_t cblocks)
+{
+	if (direction != BJXA_HIP_OFFLOAD_DECODE &&
+	    direction != BJXA_HIP_OFFLOAD_ENCODE) {
+		errno = EINVAL;
+		return (-1);
+	}
+	(void)pthread_once(&offload_once, offload_init);
+	if (cblocks < 0)
+		return ((int64_t)__atomic_load_n(&offload_min[direction],
+		    __ATOMIC_RELAXED));
+	return ((int64_t)__atomic_exchange_n(&offload_min[direction],
+	    (uint64_t)cblocks, __ATOMIC_RELAXED));
 }
 
 /* ---- objects (src/libbjxa.c:246-282) --------------------------------- */
@@ -309,12 +370,17 @@ bjxa_decode(bjxa_decoder_t *dec, void *dst, size_t dst_len, const void *src,
 	if (copy > f->data_len_pcm)
 		copy = f->data_len_pcm;
 
-	if (dec->gpu == NULL && (dec->gpu = bjxa__gpu_new()) == NULL)
-		return (-1);
 	memcpy(st, dec->state, sizeof st);
-	if (bjxa__gpu_decode(dec->gpu, src, (uint32_t)n, dec->bits,
-	    dec->channels, st, dst, copy, &err_cb) < 0)
-		return (-1);
+	if (!on_gpu(BJXA_HIP_OFFLOAD_DECODE, n * dec->channels)) {
+		(void)bjxa__cpu_decode(src, (uint32_t)n, dec->bits,
+		    dec->channels, st, dst, copy, &err_cb);
+	} else {
+		if (dec->gpu == NULL && (dec->gpu = bjxa__gpu_new()) == NULL)
+			return (-1);
+		if (bjxa__gpu_decode(dec->gpu, src, (uint32_t)n, dec->bits,
+		    dec->channels, st, dst, copy, &err_cb) < 0)
+			return (-1);
+	}
 	memcpy(dec->state, st, sizeof st);
 	if (err_cb != 0xffffffffu) {
 		/* gain nibble >= 5 (:550): the eblocks before it are in dst
@@ -552,11 +618,16 @@ bjxa_encode(bjxa_encoder_t *enc, void *dst, size_t dst_len, const void *src,
 	frames = (n - 1) * XA_FRAMES + (take - (n - 1) * f->block_size_pcm) /
 	    (enc->channels * 2u);
 
-	if (enc->gpu == NULL && (enc->gpu = bjxa__gpu_new()) == NULL)
-		return (-1);
-	if (bjxa__gpu_encode(enc->gpu, src, frames, enc->bits, enc->channels,
-	    dst) < 0)
-		return (-1);
+	if (!on_gpu(BJXA_HIP_OFFLOAD_ENCODE, n * enc->channels)) {
+		(void)bjxa__cpu_encode(src, frames, enc->bits, enc->channels,
+		    dst);
+	} else {
+		if (enc->gpu == NULL && (enc->gpu = bjxa__gpu_new()) == NULL)
+			return (-1);
+		if (bjxa__gpu_encode(enc->gpu, src, frames, enc->bits,
+		    enc->channels, dst) < 0)
+			return (-1);
+	}
 	f->blocks -= (uint32_t)n;
 	f->data_len_pcm -= (uint32_t)take;
 	return ((int)n);

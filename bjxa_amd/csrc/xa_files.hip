@@ -166,6 +166,8 @@ struct files_ctx {
 	uint8_t *d_in = NULL, *d_out = NULL;
 	uint32_t *d_st = NULL;
 	size_t in_cap = 0, out_cap = 0, st_cap = 0;
+	void *d_bws = NULL;			/* batch workspace, kept */
+	size_t bws_cap = 0;
 	copy_pool *pool = NULL;
 };
 
@@ -313,8 +315,8 @@ bjxa__gpu_decode_many(struct bjxa__job *jobs, uint32_t n)
 	}
 	TMARK("h2d");
 	{
-		bjxa_hip_batch_t *b = bjxa_hip_batch_new(hs.data(), n, NULL,
-		    c.stream);
+		bjxa_hip_batch_t *b = bjxa__batch_new(hs.data(), n, NULL,
+		    c.stream, &c.d_bws, &c.bws_cap);
 		if (b == NULL)
 			return -1;
 		const int r = bjxa_hip_batch_decode_async(b, c.d_st, NULL,

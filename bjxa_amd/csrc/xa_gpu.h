@@ -8,6 +8,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "bjxa_hip.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -50,9 +52,25 @@ struct bjxa__job {
  */
 int bjxa__gpu_decode_many(struct bjxa__job *jobs, uint32_t n);
 
+/* bjxa_hip_batch_new in a device workspace the caller keeps across
+ * batches (grown in place; not freed by bjxa_hip_batch_free) */
+bjxa_hip_batch_t *bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
+    const bjxa_hip_tuning_t *tune, void *stream, void **ws_cache,
+    size_t *ws_cap);
+
 /* encode `frames` frames from host `src` into ceil(frames/32) eblocks */
 int bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
     unsigned bits, unsigned ch, void *dst);
+
+/*
+ * CPU core (xa_cpu.c): the same contracts as bjxa__gpu_decode and
+ * bjxa__gpu_encode, on the calling thread; they cannot fail.
+ */
+int bjxa__cpu_decode(const void *src, uint32_t eblocks, unsigned bits,
+    unsigned ch, int16_t state[4], void *dst, uint64_t dst_bytes,
+    uint32_t *err_cb);
+int bjxa__cpu_encode(const void *src, uint64_t frames, unsigned bits,
+    unsigned ch, void *dst);
 
 #ifdef __cplusplus
 }

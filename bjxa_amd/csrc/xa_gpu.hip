@@ -11,6 +11,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "xa_decode.h"
 #include "xa_gpu.h"
 #include "../../include/bjxa_hip.h"
@@ -18,26 +20,50 @@
 #define DEFAULT_WARMUP	8u	/* eblocks; DESIGN.md §3 */
 #define MIN_CHUNK	16u
 /*
- * Automatic chunking: about TARGET_LANES chunks -- two resident 256-lane
- * workgroups on each of the 256 CUs, whose memory pipelines bound the
- * speculative kernel.  Uniform chunks of ceil(eblocks / TARGET_LANES)
- * rounded up to the group measured best (C3: 40 eblocks, 489 workgroups;
- * C2: 80); an exactly balanced plan of 512 workgroups with two chunk
- * lengths (XA_VARIANT_BALANCED) was 12 % slower ("Tuning").
+ * Automatic chunking: about target_lanes() chunks -- two resident 256-lane
+ * workgroups on each CU of the current device (256 on MI355X), whose
+ * memory pipelines bound the speculative kernel.  Uniform chunks of
+ * ceil(eblocks / lanes) rounded up to the group measured best (C3: 40
+ * eblocks, 489 workgroups; C2: 80); an exactly balanced plan of 512
+ * workgroups with two chunk lengths (XA_VARIANT_BALANCED) was 12 % slower
+ * ("Tuning").
  */
-#define TARGET_LANES	(256u * 2u * 256u)
+#define MAX_DEVICES	64
 #define XA_VARIANT_STRUCT	0xfu	/* kernel structure, 0 = automatic */
 #define XA_VARIANT_BALANCED	0x20u	/* two-length chunk plan */
 
+/* a HIP device is visible; probed once per process, thread-safe */
 extern "C" int
 bjxa__gpu_present(void)
 {
-	static int state;	/* 0 unknown, 1 yes, -1 no */
-	if (state == 0) {
+	static std::once_flag once;
+	static int present;
+	std::call_once(once, [] {
 		int n = 0;
-		state = (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : -1;
+		present = hipGetDeviceCount(&n) == hipSuccess && n > 0;
+	});
+	return present;
+}
+
+/* 2 x 256 lanes per CU of the current device (CU count read once per
+ * device; 256 CUs if the query fails) */
+static uint32_t
+target_lanes(void)
+{
+	static uint32_t cus[MAX_DEVICES];	/* 0 = not read yet */
+	int dev = 0, n = 0;
+	uint32_t c;
+
+	if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES)
+		dev = -1;
+	c = dev >= 0 ? __atomic_load_n(&cus[dev], __ATOMIC_RELAXED) : 0;
+	if (c == 0) {
+		c = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount,
+		    dev < 0 ? 0 : dev) == hipSuccess && n > 0) ? (uint32_t)n : 256u;
+		if (dev >= 0)
+			__atomic_store_n(&cus[dev], c, __ATOMIC_RELAXED);
 	}
-	return state > 0;
+	return c * 2u * 256u;
 }
 
 static uint32_t
@@ -54,7 +80,7 @@ struct plan {
 
 /*
  * Chunk plan for one stream.  Automatic: uniform chunks (above).  With
- * XA_VARIANT_BALANCED: exactly TARGET_LANES chunks once the stream is long
+ * XA_VARIANT_BALANCED: exactly target_lanes() chunks once the stream is long
  * enough, C = eblocks per lane rounded down to the chunk quantum (G =
  * XA_CHUNK_Q(ch) eblocks) and the remainder spread as whole quanta over the leading
  * chunks, rounded up to whole waves so every wave has one chunk length.
@@ -64,7 +90,7 @@ static void
 plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
     struct plan *p)
 {
-	const uint32_t G = XA_CHUNK_Q(ch);
+	const uint32_t G = XA_CHUNK_Q(ch), lanes = target_lanes();
 	const uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup :
 	    DEFAULT_WARMUP;
 	uint32_t c;
@@ -73,15 +99,14 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 	if (t && t->chunk) {
 		c = t->chunk;
 	} else if (!(t && (t->variant & XA_VARIANT_BALANCED))) {
-		c = (uint32_t)(((uint64_t)eblocks + TARGET_LANES - 1) /
-		    TARGET_LANES);
+		c = (uint32_t)(((uint64_t)eblocks + lanes - 1) / lanes);
 		if (c < MIN_CHUNK)
 			c = MIN_CHUNK;
 	} else {
-		c = eblocks / TARGET_LANES / G * G;
+		c = eblocks / lanes / G * G;
 		if (c >= MIN_CHUNK) {
 			const uint64_t rest = (uint64_t)eblocks -
-			    (uint64_t)TARGET_LANES * c;
+			    (uint64_t)lanes * c;
 			const uint32_t nl = round_up((uint32_t)((rest + G - 1) / G),
 			    64u);
 			const uint64_t cover = (uint64_t)nl * (c + G);
@@ -242,6 +267,9 @@ bjxa_hip_encode_async(const void *d_pcm, uint64_t frames, unsigned bits,
 
 struct bjxa_hip_batch {
 	void		*d_ws;
+	bool		owns_ws;	/* false: a workspace lent by the caller */
+	bool		launched;	/* `done` has been recorded */
+	hipEvent_t	done;		/* after the last decode's kernels */
 	xa_batch_args	args;
 };
 
@@ -279,7 +307,7 @@ stream_ok(const bjxa_hip_stream_t *s)
 
 /*
  * Plan: one budget of channel blocks per lane, Cb = the batch's channel
- * blocks / TARGET_LANES (at least MIN_CHUNK, a multiple of 4); a stream of
+ * blocks / target_lanes() (at least MIN_CHUNK, a multiple of 4); a stream of
  * E eblocks and ch channels gets k = round(E*ch / (64*Cb)) >= 1 whole
  * waves and chunks of ceil(E / 64k) eblocks (rounded up to its group, at
  * least MIN_CHUNK), so a stereo lane decodes about Cb/2 eblocks and a mono
@@ -288,6 +316,20 @@ stream_ok(const bjxa_hip_stream_t *s)
 extern "C" bjxa_hip_batch_t *
 bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
     const bjxa_hip_tuning_t *tune, void *stream)
+{
+	return bjxa__batch_new(s, n, tune, stream, NULL, NULL);
+}
+
+/*
+ * bjxa_hip_batch_new, optionally in a workspace the caller keeps across
+ * batches (*ws_cache of *ws_cap bytes, grown here when too small; the
+ * batch then does not free it).  The files path uses this so that a call
+ * does not allocate and free device memory.
+ */
+extern "C" bjxa_hip_batch_t *
+bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
+    const bjxa_hip_tuning_t *tune, void *stream, void **ws_cache,
+    size_t *ws_cap)
 {
 	if (s == NULL || n == 0) {
 		errno = EINVAL;
@@ -305,7 +347,8 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		errno = ENODEV;
 		return NULL;
 	}
-	uint64_t cb = (cblocks + TARGET_LANES - 1) / TARGET_LANES;
+	const uint32_t lanes = target_lanes();
+	uint64_t cb = (cblocks + lanes - 1) / lanes;
 	if (tune && tune->chunk)
 		cb = tune->chunk;
 	if (cb < MIN_CHUNK)
@@ -372,14 +415,40 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	const size_t o_q = o_e + nc * 8;
 	const size_t len = o_q + 2 * nc * 4;
 	uint8_t *ws = NULL;
-	if (hipMalloc((void **)&ws, len) != hipSuccess) {
+	if (ws_cache != NULL && *ws_cap >= len) {
+		ws = (uint8_t *)*ws_cache;
+	} else {
+		if (ws_cache != NULL) {
+			/* the previous user of the cache has completed */
+			(void)hipStreamSynchronize((hipStream_t)stream);
+			(void)hipFree(*ws_cache);
+			*ws_cache = NULL;
+			*ws_cap = 0;
+		}
+		if (hipMalloc((void **)&ws, len) != hipSuccess) {
+			free(hs);
+			free(hw);
+			free(b);
+			errno = ENOMEM;
+			return NULL;
+		}
+		if (ws_cache != NULL) {
+			*ws_cache = ws;
+			*ws_cap = len;
+		}
+	}
+	b->d_ws = ws;
+	b->owns_ws = ws_cache == NULL;
+	if (hipEventCreateWithFlags(&b->done, hipEventDisableTiming) !=
+	    hipSuccess) {
+		if (b->owns_ws)
+			(void)hipFree(ws);
 		free(hs);
 		free(hw);
 		free(b);
-		errno = ENOMEM;
+		errno = EIO;
 		return NULL;
 	}
-	b->d_ws = ws;
 	xa_batch_args &a = b->args;
 	a.streams = (const xa_batch_stream *)(ws + o_str);
 	a.wstream = (const uint32_t *)(ws + o_wav);
@@ -392,10 +461,13 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	a.ctl = (uint32_t *)ws;
 	a.sctl = (uint32_t *)(ws + o_sctl);
 	a.status = NULL;
-	int bad = hipMemcpy(ws + o_str, hs, (size_t)n * sizeof *hs,
-	    hipMemcpyHostToDevice) != hipSuccess ||
-	    hipMemcpy(ws + o_wav, hw, nwaves * 4, hipMemcpyHostToDevice) !=
-	    hipSuccess;
+	/* stream-ordered uploads: the workspace may still be in use by an
+	 * earlier batch on the same stream (the files path) */
+	int bad = hipMemcpyAsync(ws + o_str, hs, (size_t)n * sizeof *hs,
+	    hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess ||
+	    hipMemcpyAsync(ws + o_wav, hw, nwaves * 4, hipMemcpyHostToDevice,
+	    (hipStream_t)stream) != hipSuccess ||
+	    hipStreamSynchronize((hipStream_t)stream) != hipSuccess;
 	free(hs);
 	free(hw);
 	if (!bad) {
@@ -404,7 +476,9 @@ bjxa_hip_batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		bad = hipGetLastError() != hipSuccess;
 	}
 	if (bad) {
-		(void)hipFree(ws);
+		(void)hipEventDestroy(b->done);
+		if (b->owns_ws)
+			(void)hipFree(ws);
 		free(b);
 		errno = EIO;
 		return NULL;
@@ -423,20 +497,26 @@ bjxa_hip_batch_decode_async(bjxa_hip_batch_t *b, uint32_t *d_status,
 	b->args.status = d_status;
 	if (xa_decode_batch_launch(b->args, (hipStream_t)stream,
 	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
-	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
+	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess ||
+	    hipEventRecord(b->done, (hipStream_t)stream) != hipSuccess) {
 		errno = EIO;
 		return -1;
 	}
+	b->launched = true;
 	return 0;
 }
 
+/* waits for the batch's own last decode only (not the whole device) */
 extern "C" void
 bjxa_hip_batch_free(bjxa_hip_batch_t *b)
 {
 	if (b == NULL)
 		return;
-	(void)hipDeviceSynchronize();
-	(void)hipFree(b->d_ws);
+	if (b->launched)
+		(void)hipEventSynchronize(b->done);
+	(void)hipEventDestroy(b->done);
+	if (b->owns_ws)
+		(void)hipFree(b->d_ws);
 	free(b);
 }
 
@@ -450,6 +530,7 @@ bjxa_hip_version(void)
 /* per-codec GPU context behind bjxa_decode()/bjxa_encode()            */
 
 struct bjxa__gpu {
+	int		device;		/* current HIP device at creation */
 	hipStream_t	stream;
 	void		*d_in, *d_out, *d_ws;
 	size_t		in_cap, out_cap, ws_cap;
@@ -477,6 +558,27 @@ grow(void **p, size_t *cap, size_t need)
 	return 0;
 }
 
+/*
+ * A codec is bound to the HIP device that is current on the thread that
+ * first runs it on the GPU; every later call switches the calling thread
+ * to that device for the call's duration and back (so a codec created
+ * under hipSetDevice(k) keeps using GPU k from any thread).
+ */
+struct device_scope {
+	int	prev;
+	bool	moved;
+	explicit device_scope(int dev) : prev(-1), moved(false)
+	{
+		if (hipGetDevice(&prev) == hipSuccess && prev != dev)
+			moved = hipSetDevice(dev) == hipSuccess;
+	}
+	~device_scope()
+	{
+		if (moved)
+			(void)hipSetDevice(prev);
+	}
+};
+
 extern "C" struct bjxa__gpu *
 bjxa__gpu_new(void)
 {
@@ -489,6 +591,8 @@ bjxa__gpu_new(void)
 		errno = ENOMEM;
 		return NULL;
 	}
+	if (hipGetDevice(&g->device) != hipSuccess)
+		g->device = 0;
 	if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) !=
 	    hipSuccess || hipMalloc((void **)&g->d_status, 64) != hipSuccess) {
 		free(g);
@@ -503,6 +607,7 @@ bjxa__gpu_free(struct bjxa__gpu *g)
 {
 	if (g == NULL)
 		return;
+	device_scope on(g->device);
 	(void)hipStreamSynchronize(g->stream);
 	(void)hipFree(g->d_in);
 	(void)hipFree(g->d_out);
@@ -580,6 +685,7 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
     unsigned bits, unsigned ch, int16_t state[4], void *dst,
     uint64_t dst_bytes, uint32_t *err_cb)
 {
+	device_scope on(g->device);
 	if (eblocks <= XA_SMALL_MAX)
 		return small_decode(g, src, eblocks, bits, ch, state, dst,
 		    dst_bytes, err_cb);
@@ -664,6 +770,7 @@ bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
 	const size_t in_bytes = (size_t)frames * 2u * ch;
 	const uint32_t eblocks = (uint32_t)((frames + 31) / 32);
 	const size_t out_bytes = (size_t)eblocks * (bits * 4 + 1) * ch;
+	device_scope on(g->device);
 
 	if (eblocks <= XA_SMALL_MAX) {
 		/* one launch over the pinned buffer */

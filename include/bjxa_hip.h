@@ -131,6 +131,20 @@ typedef struct {
 int bjxa_hip_parse_headers_async(const void *d_src, size_t stride, uint32_t n,
     bjxa_hip_header_t *d_out, void *stream);
 
+/*
+ * Routing of the host API (LIBBJXA_HIP_0.3).  bjxa_decode()/bjxa_encode()
+ * run a call of at least `cblocks` channel blocks (eblocks x channels) on
+ * the GPU and a smaller one on the calling thread's CPU core; without a
+ * GPU every call runs on the CPU.  0 sends every call to the GPU,
+ * INT64_MAX none.  cblocks < 0 only queries.  Returns the previous
+ * threshold, or -1/EINVAL for an unknown direction.  Process-wide,
+ * thread-safe; the defaults (measured crossover points) can
+ * be overridden with BJXA_OFFLOAD_DECODE / BJXA_OFFLOAD_ENCODE.
+ */
+#define BJXA_HIP_OFFLOAD_DECODE	0
+#define BJXA_HIP_OFFLOAD_ENCODE	1
+int64_t bjxa_hip_offload_threshold(int direction, int64_t cblocks);
+
 /* library/kernels build identifier, e.g. "bjxa-mi355x gfx950 ..." */
 const char *bjxa_hip_version(void);
 

@@ -3,9 +3,14 @@
  * checks of the reference's test/test_libbjxa_api.c:40-296, run against
  * the MI355X libbjxa.so.0.
  *
- * usage: test_api <golden-dir> [gpu]
- *   The decode cases that need the kernels run only with "gpu"; without it
- *   bjxa_decode() must fail with ENODEV once its argument checks pass.
+ * usage: test_api <golden-dir> [<wav-out>]
+ *   Every case runs the same with or without a GPU: small calls go to the
+ *   library's CPU core, and without a GPU every call does (the test that
+ *   runs this under -m gpu sets BJXA_OFFLOAD_DECODE/ENCODE=0 to send the
+ *   same calls to the kernels).  With <wav-out>, the mono 4-bit fixture is
+ *   also decoded one block per call -- the reference CLI's default loop,
+ *   src/bjxa_decode.c:102-155 -- into that WAV file, whose SHA-1 the caller
+ *   checks against test/test_decode.sh's.
  */
 #ifdef NDEBUG
 #undef NDEBUG
@@ -26,7 +31,6 @@
 static const char junk_text[] = "random junk";
 static char src_buf[4096];
 static char dst_buf[4096];
-static int have_gpu;
 static const char *golden;
 
 /* the mono 4-bit fixture's header (the reference opens test/square-mono-4.xa) */
@@ -131,21 +135,17 @@ check_decoding(void)
 	    errno == ENOBUFS);
 	assert(bjxa_decode_format(dec, &fmt) == 0);
 
-	if (!have_gpu) {
-		assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm, src_buf,
-		    fmt.block_size_xa) == -1 && errno == ENODEV);
-	} else {
-		/* dst room for 2 blocks, src for 1 -> 1; and the converse */
-		assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm * 2,
-		    src_buf, fmt.block_size_xa) == 1);
-		assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm,
-		    src_buf, fmt.block_size_xa * 2) == 1);
-		/* past the last block */
-		while (bjxa_decode(dec, dst_buf, fmt.block_size_pcm, src_buf,
-		    fmt.block_size_xa) == 1)
-			;
-		assert(errno == EPROTO);
-	}
+	/* dst room for 2 blocks, src for 1 -> 1; and the converse */
+	memset(src_buf, 0, sizeof src_buf);
+	assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm * 2,
+	    src_buf, fmt.block_size_xa) == 1);
+	assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm,
+	    src_buf, fmt.block_size_xa * 2) == 1);
+	/* past the last block */
+	while (bjxa_decode(dec, dst_buf, fmt.block_size_pcm, src_buf,
+	    fmt.block_size_xa) == 1)
+		;
+	assert(errno == EPROTO);
 	assert(bjxa_free_decoder(&dec) == 0);
 	free(junk);
 	fclose(file);
@@ -236,13 +236,40 @@ check_encoder(void)
 	    errno == ENOBUFS);
 	assert(bjxa_encode(enc, dst_buf, 50, src_buf, 127) == -1 &&
 	    errno == ENOBUFS);
-	if (!have_gpu)
-		assert(bjxa_encode(enc, dst_buf, 50, src_buf, 128) == -1 &&
-		    errno == ENODEV);
-	else
-		assert(bjxa_encode(enc, dst_buf, 200, src_buf, 400) == 4);
+	assert(bjxa_encode(enc, dst_buf, 200, src_buf, 400) == 4);
 	assert(bjxa_free_encoder(&enc) == 0);
 	free(junk);
+}
+
+/* the fixture through one bjxa_decode() per block into a WAV file */
+static void
+decode_fixture(const char *path)
+{
+	bjxa_decoder_t *dec = bjxa_decoder();
+	bjxa_format_t fmt;
+	FILE *in = open_fixture(), *out = fopen(path, "wb");
+	uint32_t left;
+
+	assert(dec != NULL && out != NULL);
+	assert(bjxa_fread_header(dec, in) == 32);
+	assert(bjxa_decode_format(dec, &fmt) == 0);
+	assert(bjxa_fwrite_riff_header(dec, out) == 44);
+	left = fmt.data_len_pcm;
+	while (fmt.blocks-- > 0) {
+		const uint32_t n = left < fmt.block_size_pcm ? left :
+		    fmt.block_size_pcm;
+		assert(fread(src_buf, fmt.block_size_xa, 1, in) == 1);
+		assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm, src_buf,
+		    fmt.block_size_xa) == 1);
+		assert(bjxa_fwrite_pcm((int16_t *)(void *)dst_buf, n, out) == 0);
+		left -= n;
+	}
+	assert(left == 0);
+	assert(bjxa_decode(dec, dst_buf, fmt.block_size_pcm, src_buf,
+	    fmt.block_size_xa) == -1 && errno == EPROTO);
+	assert(bjxa_free_decoder(&dec) == 0);
+	fclose(in);
+	assert(fclose(out) == 0);
 }
 
 int
@@ -250,7 +277,6 @@ main(int argc, char **argv)
 {
 	assert(argc >= 2);
 	golden = argv[1];
-	have_gpu = argc > 2 && strcmp(argv[2], "gpu") == 0;
 	assert(sizeof(bjxa_format_t) == 16);
 	check_memory_management();
 	check_header_parsing();
@@ -259,6 +285,8 @@ main(int argc, char **argv)
 	check_riff_header_dumping();
 	check_pcm_samples_dumping();
 	check_encoder();
+	if (argc > 2)
+		decode_fixture(argv[2]);
 	puts("test_api: ok");
 	return (EXIT_SUCCESS);
 }

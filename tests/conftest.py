@@ -21,6 +21,22 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP kernels)")
+    config.addinivalue_line("markers", "routing: a GPU test that keeps the library's default "
+                            "CPU/GPU routing of host-API calls")
+
+
+@pytest.fixture(autouse=True)
+def _gpu_route(request):
+    """GPU tests drive the host API's calls to the kernels (offload threshold
+    0) unless marked `routing`; CPU tests leave the routing alone (without a
+    GPU every call runs on the CPU core anyway)."""
+    if "gpu" in request.keywords and "routing" not in request.keywords:
+        import bjxa_amd
+        if os.path.exists(bjxa_amd.LIB_PATH):
+            with bjxa_amd.offload(0):
+                yield
+            return
+    yield
 
 
 @pytest.fixture(scope="session")

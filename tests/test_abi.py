@@ -77,14 +77,20 @@ def build_api_test(built, tmp_path):
     return str(exe)
 
 
-def test_c_api_contract_cpu(built, tmp_path):
-    """Argument/errno checks; decode/encode end in ENODEV without a GPU."""
+def test_c_api_contract_cpu(built, manifest, tmp_path):
+    """Argument/errno checks of test/test_libbjxa_api.c, and the fixture
+    decoded one block per call, on a host with no GPU visible: every call
+    runs on the library's CPU core."""
+    import hashlib
     exe = build_api_test(built, tmp_path)
     env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
-    r = subprocess.run([exe, GOLDEN], stdin=subprocess.DEVNULL, capture_output=True,
+    wav = tmp_path / "out.wav"
+    r = subprocess.run([exe, GOLDEN, str(wav)], stdin=subprocess.DEVNULL, capture_output=True,
                        text=True, env=env)
     assert r.returncode == 0, r.stderr
     assert "test_api: ok" in r.stdout
+    sha = hashlib.sha1(wav.read_bytes()).hexdigest()
+    assert sha == manifest["fixtures"]["square-mono-4.xa"]["wav_sha1"]
 
 
 @pytest.mark.parametrize("case", range(11))

@@ -151,3 +151,53 @@ def test_single_stream_split(world, eb, bits, ch, mix, warmup):
         assert tuple(r[2])[:2 * ch] == tuple(st_ref)[:2 * ch]
     if mix == "W" and eb > 100:
         assert any(r[3] > 1 for r in res)      # some rank had to re-decode
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BJXA_BENCH_BACKEND="gloo", HIP_VISIBLE_DEVICES="-1")
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                       capture_output=True, text=True, env=env, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.parametrize("world,streams", [(2, 7), (3, 8)])
+def test_bench_launcher_spawns_ranks(world, streams):
+    """`bench.py --gpus N` with no WORLD_SIZE starts N ranks itself (child
+    torch.distributed.run, same code path as on the GPU box but over gloo):
+    the line reports n_gpus == N, the shards tile the job, and the
+    AllGather'ed per-stream checksums match the oracle's on rank 0."""
+    rc, line, err = _bench(["--gpus", str(world), "--streams", str(streams), "--eblocks", "300",
+                            "--steps", "1", "--warmup", "0"])
+    assert rc == 0, err[-3000:]
+    assert line["n_gpus"] == world and line["scaling"] == "strong"
+    cp = line["control_plane"]
+    shards = cp["shards"]
+    assert len(shards) == world and shards[0][0] == 0 and shards[-1][1] == streams
+    assert all(a[1] == b[0] for a, b in zip(shards, shards[1:]))
+    assert line["config"]["streams"] == streams
+    assert cp["samples"] == streams * 300 * 64
+    assert line["bit_exact"] is True and cp["checksums_match_oracle"] is True
+    assert cp["first_error_stream"] is None
+
+
+def test_bench_first_error_collective():
+    """AllReduce(min) of the first failing stream: stream 5 of 8 carries a
+    gain-5 profile; every stream's checksum (the failed one's up to its
+    failing eblock) still matches the oracle's."""
+    rc, line, err = _bench(["--gpus", "2", "--streams", "8", "--eblocks", "200",
+                            "--steps", "1", "--warmup", "0", "--bad-stream", "5"])
+    assert rc == 0, err[-3000:]
+    assert line["control_plane"]["first_error_stream"] == 5
+    assert line["control_plane"]["checksums_match_oracle"] is True
+
+
+def test_bench_world_mismatch():
+    """A rank whose WORLD_SIZE disagrees with --gpus refuses to report."""
+    rc, line, err = _bench(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc == 2 and line is None and "WORLD_SIZE=1" in err

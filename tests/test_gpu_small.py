@@ -1,7 +1,9 @@
-"""The host API's low-latency path for small calls (<= 32 eblocks per
-bjxa_decode/bjxa_encode, bjxa_amd/csrc/xa_small.hip) and its hand-over to
-the bulk path: every format, call sizes on both sides of the threshold,
-state carried across calls, the reference's error semantics."""
+"""The host API's GPU paths for small calls (<= 32 eblocks per
+bjxa_decode/bjxa_encode, bjxa_amd/csrc/xa_small.hip, reached with the
+offload threshold at 0) and the bulk path, and the default routing that
+sends calls below the offload threshold to the CPU core and larger ones to
+the GPU: every format, call sizes on both sides of each threshold, state
+carried across calls, the reference's error semantics."""
 import errno
 
 import numpy as np
@@ -87,6 +89,66 @@ def test_small_encode_calls(built, bits, ch):
     out, pos = bytearray(), 0
     while pos < fmt["blocks"]:
         n = min(int(rng.integers(1, 41)), fmt["blocks"] - pos)
+        chunk = np.frombuffer(raw[pos * bp:(pos + n) * bp].ljust(n * bp, b"\0"),
+                              np.uint8).copy()
+        dst = np.zeros(n * bx, np.uint8)
+        assert e.encode(dst, chunk) == n
+        out += dst.tobytes()
+        pos += n
+    e.close()
+    assert bytes(out) == oracle.encode(pcm, frames, bits, ch).tobytes()
+
+
+@pytest.mark.routing
+@pytest.mark.parametrize("bits,ch", FORMATS)
+def test_default_routing_chain(built, bits, ch):
+    """Default routing: calls below the decode offload threshold run on the
+    CPU core, larger ones on the GPU, through one decoder; the chained
+    output equals the single-pass oracle (state handed back and forth)."""
+    thr = bjxa_amd.offload_threshold(bjxa_amd.OFFLOAD_DECODE)
+    assert 0 < thr < 1 << 20
+    rng = np.random.default_rng(300 + bits * 10 + ch)
+    top = 3 * thr // ch + 2
+    sizes = [int(v) for v in rng.integers(1, top, 24)] + [1, 2, thr // ch, thr // ch + 1]
+    eb = sum(sizes)
+    frames = eb * 32 - 5
+    state = (-1, 2, -3, 4)
+    xa = synth.stream(eb, bits, ch, "W", seed=bits * 3 + ch)
+    hdr = bjxa_amd.xa_header(xa.size, frames, 44100, bits, ch, state)
+    ref, _, _, _ = oracle.decode(xa, eb, bits, ch, state, frames)
+    bx = (bits * 4 + 1) * ch
+    out = bytearray()
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(hdr)
+        pos, left = 0, frames * ch * 2
+        for n in sizes:
+            dst = np.zeros(n * 64 * ch, np.uint8)
+            assert d.decode(dst, xa[pos * bx:(pos + n) * bx].copy()) == n
+            take = min(n * 64 * ch, left)
+            out += dst[:take].tobytes()
+            left -= take
+            pos += n
+    assert bytes(out) == ref.tobytes()
+
+
+@pytest.mark.routing
+@pytest.mark.parametrize("bits,ch", FORMATS)
+def test_default_routing_encode(built, bits, ch):
+    """Encode calls on both sides of the encode offload threshold."""
+    thr = bjxa_amd.offload_threshold(bjxa_amd.OFFLOAD_ENCODE)
+    rng = np.random.default_rng(400 + bits * 10 + ch)
+    sizes = [int(v) for v in rng.integers(1, 2 * thr // ch + 2, 10)] + [thr // ch + 1]
+    blocks = sum(sizes)
+    frames = blocks * 32 - 3
+    pcm = synth.pcm(frames, ch, seed=bits + 5 * ch)
+    e = bjxa_amd.Encoder()
+    fmt = e.init({"data_len_pcm": frames * 2 * ch, "blocks": 0, "block_size_pcm": 0,
+                  "block_size_xa": 0, "samples_rate": 8000, "sample_bits": 16,
+                  "channels": ch}, bits)
+    raw = pcm.tobytes()
+    bp, bx = fmt["block_size_pcm"], fmt["block_size_xa"]
+    out, pos = bytearray(), 0
+    for n in sizes:
         chunk = np.frombuffer(raw[pos * bp:(pos + n) * bp].ljust(n * bp, b"\0"),
                               np.uint8).copy()
         dst = np.zeros(n * bx, np.uint8)
