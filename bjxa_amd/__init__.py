@@ -411,11 +411,11 @@ def encode_device(d_pcm, frames, bits, channels, d_xa, stream=0):
 OFFLOAD_DECODE, OFFLOAD_ENCODE = 0, 1
 
 
-def offload_threshold(direction, cblocks=-1):
-    """bjxa_hip_offload_threshold: set (cblocks >= 0) or query the number
-    of channel blocks from which bjxa_decode/bjxa_encode run on the GPU;
-    returns the previous value."""
-    return _check(lib().bjxa_hip_offload_threshold(direction, cblocks),
+def offload_threshold(direction, eblocks=-1):
+    """bjxa_hip_offload_threshold: set (eblocks >= 0) or query the number
+    of effective blocks from which bjxa_decode/bjxa_encode calls run on the
+    GPU; returns the previous value."""
+    return _check(lib().bjxa_hip_offload_threshold(direction, eblocks),
                   "bjxa_hip_offload_threshold")
 
 
@@ -423,8 +423,8 @@ class offload:
     """Context manager routing host-API calls: offload(0) sends every call
     to the GPU, offload(None) none (CPU core only)."""
 
-    def __init__(self, cblocks):
-        self.v = (1 << 63) - 1 if cblocks is None else cblocks
+    def __init__(self, eblocks):
+        self.v = (1 << 63) - 1 if eblocks is None else eblocks
 
     def __enter__(self):
         self.old = [offload_threshold(d, self.v) for d in (OFFLOAD_DECODE, OFFLOAD_ENCODE)]

@@ -105,14 +105,17 @@ read_all(void *buf, size_t n, FILE *file)
 /* ---- CPU / GPU routing (LIBBJXA_HIP_0.3) ------------------------------- */
 
 /*
- * A call of at least offload_min[dir] channel blocks runs on the GPU,
- * a smaller one on the calling core.  Defaults are the measured crossover
- * points of tools/call_latency.py; BJXA_OFFLOAD_DECODE and
- * BJXA_OFFLOAD_ENCODE (channel blocks) override them at load time, and
- * bjxa_hip_offload_threshold() at run time.
+ * A call of at least offload_min[dir] effective blocks runs on the GPU, a
+ * smaller one on the calling core.  The unit is the eblock because the CPU
+ * core's cost is: a stereo eblock runs its two channel chains side by side
+ * in about the time of one mono block.  Defaults are the crossover points
+ * measured with tools/call_latency.c on the GPU box (EPYC 9575F host,
+ * DESIGN.md §1 "Routing": decode ~1,100 stereo / ~800 mono eblocks, encode
+ * ~4,000-5,000); BJXA_OFFLOAD_DECODE and BJXA_OFFLOAD_ENCODE override them
+ * at load time, bjxa_hip_offload_threshold() at run time.
  */
-#define OFFLOAD_DECODE_DEFAULT	2048u
-#define OFFLOAD_ENCODE_DEFAULT	8192u
+#define OFFLOAD_DECODE_DEFAULT	1024u
+#define OFFLOAD_ENCODE_DEFAULT	4096u
 
 static uint64_t offload_min[2];
 static pthread_once_t offload_once = PTHREAD_ONCE_INIT;
@@ -137,15 +140,15 @@ offload_init(void)
 }
 
 static int
-on_gpu(int dir, uint64_t cblocks)
+on_gpu(int dir, uint64_t eblocks)
 {
 	(void)pthread_once(&offload_once, offload_init);
-	return cblocks >= __atomic_load_n(&offload_min[dir], __ATOMIC_RELAXED) &&
+	return eblocks >= __atomic_load_n(&offload_min[dir], __ATOMIC_RELAXED) &&
 	    bjxa__gpu_present();
 }
 
 int64_t
-bjxa_hip_offload_threshold(int direction, int64_t cblocks)
+bjxa_hip_offload_threshold(int direction, int64_t eblocks)
 {
 	if (direction != BJXA_HIP_OFFLOAD_DECODE &&
 	    direction != BJXA_HIP_OFFLOAD_ENCODE) {
@@ -153,11 +156,11 @@ bjxa_hip_offload_threshold(int direction, int64_t cblocks)
 		return (-1);
 	}
 	(void)pthread_once(&offload_once, offload_init);
-	if (cblocks < 0)
+	if (eblocks < 0)
 		return ((int64_t)__atomic_load_n(&offload_min[direction],
 		    __ATOMIC_RELAXED));
 	return ((int64_t)__atomic_exchange_n(&offload_min[direction],
-	    (uint64_t)cblocks, __ATOMIC_RELAXED));
+	    (uint64_t)eblocks, __ATOMIC_RELAXED));
 }
 
 /* ---- objects (src/libbjxa.c:246-282) --------------------------------- */
@@ -371,7 +374,7 @@ bjxa_decode(bjxa_decoder_t *dec, void *dst, size_t dst_len, const void *src,
 		copy = f->data_len_pcm;
 
 	memcpy(st, dec->state, sizeof st);
-	if (!on_gpu(BJXA_HIP_OFFLOAD_DECODE, n * dec->channels)) {
+	if (!on_gpu(BJXA_HIP_OFFLOAD_DECODE, n)) {
 		(void)bjxa__cpu_decode(src, (uint32_t)n, dec->bits,
 		    dec->channels, st, dst, copy, &err_cb);
 	} else {
@@ -618,7 +621,7 @@ bjxa_encode(bjxa_encoder_t *enc, void *dst, size_t dst_len, const void *src,
 	frames = (n - 1) * XA_FRAMES + (take - (n - 1) * f->block_size_pcm) /
 	    (enc->channels * 2u);
 
-	if (!on_gpu(BJXA_HIP_OFFLOAD_ENCODE, n * enc->channels)) {
+	if (!on_gpu(BJXA_HIP_OFFLOAD_ENCODE, n)) {
 		(void)bjxa__cpu_encode(src, frames, enc->bits, enc->channels,
 		    dst);
 	} else {

@@ -111,3 +111,45 @@ def test_batch_c5_shape(built):
     pcms, st = run_batch(specs)
     check(specs, pcms, st)
     assert (st[:, 6] == 16).all()      # 32 x 131072 channel blocks over 131072 lanes, / 2
+
+
+def test_batch_c4_full_size(built):
+    """BASELINE config C4 at full size in one launch: 1024 streams, stream i
+    with bits (4,6,8)[i%3], channels 1+((i/3)&1), 16,384 eblocks, seeded as
+    bench.py seeds them; every stream bit-exact against the oracle (decoded
+    on 8 host threads) and its exit state equal."""
+    import threading
+    torch = require_gpu()
+    import bench
+    inputs = bench.batch_inputs("C4", 0, 0, 0, 1024)
+    assert len(inputs) == 1024
+    srcs, dsts, streams = [], [], []
+    for i, bits, ch, eb, xa in inputs:
+        s = torch.from_numpy(xa).cuda()
+        d = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+        srcs.append(s)
+        dsts.append(d)
+        streams.append({"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
+                        "bits": bits, "channels": ch})
+    status = torch.zeros(1024 * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    with bjxa_amd.Batch(streams, stream=sh) as b:
+        b.decode(status.data_ptr(), sh)
+        torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint32).reshape(1024, -1)
+    bad = []
+
+    def work(k):
+        for j in range(k, 1024, 8):
+            i, bits, ch, eb, xa = inputs[j]
+            ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch)
+            got = dsts[j].cpu().numpy().view(np.int16)
+            if (not np.array_equal(got, ref) or st[j][0] != bjxa_amd.NO_ERROR or
+                    status_state(st[j])[:2 * ch] != st_ref[:2 * ch]):
+                bad.append(i)
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not bad, bad[:10]

@@ -108,8 +108,7 @@ def test_default_routing_chain(built, bits, ch):
     thr = bjxa_amd.offload_threshold(bjxa_amd.OFFLOAD_DECODE)
     assert 0 < thr < 1 << 20
     rng = np.random.default_rng(300 + bits * 10 + ch)
-    top = 3 * thr // ch + 2
-    sizes = [int(v) for v in rng.integers(1, top, 24)] + [1, 2, thr // ch, thr // ch + 1]
+    sizes = [int(v) for v in rng.integers(1, 3 * thr, 24)] + [1, 2, thr - 1, thr]
     eb = sum(sizes)
     frames = eb * 32 - 5
     state = (-1, 2, -3, 4)
@@ -137,7 +136,7 @@ def test_default_routing_encode(built, bits, ch):
     """Encode calls on both sides of the encode offload threshold."""
     thr = bjxa_amd.offload_threshold(bjxa_amd.OFFLOAD_ENCODE)
     rng = np.random.default_rng(400 + bits * 10 + ch)
-    sizes = [int(v) for v in rng.integers(1, 2 * thr // ch + 2, 10)] + [thr // ch + 1]
+    sizes = [int(v) for v in rng.integers(1, 2 * thr, 10)] + [thr - 1, thr]
     blocks = sum(sizes)
     frames = blocks * 32 - 3
     pcm = synth.pcm(frames, ch, seed=bits + 5 * ch)
