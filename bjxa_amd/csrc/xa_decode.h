@@ -43,6 +43,8 @@ struct xa_dec_args {
 				 * XA_CHUNK_Q(ch), nlong % 64 == 0); chunk q
 				 * starts at eblock q*C + Q*min(q, nlong) */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
+	uint32_t pace;		/* K1 waves of a workgroup wait for each other
+				 * every `pace` groups (0 = never) */
 	uint2 *g, *e;		/* per-chunk entry / exit state */
 	uint32_t *queue;	/* re-check queue, nchunks entries */
 	uint32_t *ctl;		/* XA_CTL_WORDS */
@@ -82,6 +84,7 @@ struct xa_batch_args {
 	const uint32_t *wstream;	/* stream of each wave */
 	uint32_t nstreams, nwaves;	/* global chunks = 64 * nwaves */
 	uint32_t W;
+	uint32_t pace;			/* as xa_dec_args::pace */
 	uint2 *g, *e;			/* per global chunk */
 	uint32_t *queue;		/* 2 * 64 * nwaves */
 	uint32_t *ctl;			/* XA_CTL_WORDS (NQ, TICKET) */

@@ -417,7 +417,8 @@ stage_half(const xa_dec_args &a, uint8_t *land, int lane, int64_t wstart,
 
 template <int BITS, int CH, int LB, bool NT>
 __device__ __forceinline__ void
-spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
+spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
+    const uint32_t pace_every)
 {
 	typedef geo<BITS, CH> g;
 	typedef geo2<BITS, CH> g2;
@@ -547,10 +548,27 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 	 * next requests sooner (C3 spec -1.3 %, C2 -1.6 %; the stores above
 	 * or level with the DMA measured no better than without priorities) */
 	auto prio = [](auto pc) {
+#ifndef XA_NOPRIO
 		__builtin_amdgcn_s_setprio(decltype(pc)::value);
+#endif
 	};
 	/* one super-step from run `cur`, landing the next one into `nxt` */
+	/*
+	 * Pacing: every `pace_every` groups the workgroup's waves wait for
+	 * each other (a bare s_barrier, no memory fence: the LDS regions are
+	 * per wave).  Left to themselves the waves drift apart -- issue
+	 * arbitration favours the older ones -- and the early finishers leave
+	 * their CU with fewer requests in flight for the rest of the kernel;
+	 * paced, they all stream to the end (C3 spec -4 %, C2 -4.5 %,
+	 * DESIGN.md §5).  The host sets pace_every (0 = off) only when every
+	 * wave of the workgroup runs the same number of groups.
+	 */
+	auto pace = [&](int gi) {
+		if (pace_every != 0u && (uint32_t)gi % pace_every == 0u)
+			__builtin_amdgcn_s_barrier();
+	};
 	auto step = [&](int S, uint32_t *cur, uint32_t *nxt) {
+		pace(2 * S);
 		if (S == NW) {
 			gst[0] = xa_pack_state(p0[0], p1[0]);
 			gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
@@ -581,10 +599,19 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 			prio(std::integral_constant<int, 0>());
 		}
 		asm volatile("" ::: "memory");
+		pace(2 * S + 1);
 		group(cur, S, std::integral_constant<int, 1>());
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 	};
 
+#ifdef XA_DBG_TIMES
+	/* diagnostic build only: per-wave timeline (s_memrealtime, 100 MHz) --
+	 * start, end of warm-up, end -- and the XCD/SE/CU of the wave, written
+	 * into the second half of the re-check queue (tools/wave_times.py) */
+	uint32_t *trec = a.queue + a.nchunks + (wchunk0 / 64u) * 4u;
+	const uint32_t t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
+	uint32_t t_warm = t_start;
+#endif
 	uint32_t A[RD], B[RD];
 	/* prologue: super-step 0 into A, half 0 of super-step 1 in flight */
 	stage_half<BITS, CH>(a, land, lane, wstart, Cw, 0, rel_of(0), voff);
@@ -597,10 +624,30 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0)
 		stage_half<BITS, CH>(a, land, lane, wstart, Cw, 0, rel_of(1),
 		    voff);
 	for (int S = 0; S < NS; S += 2) {
+#ifdef XA_DBG_TIMES
+		if (S == NW)
+			t_warm = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
 		step(S, A, B);
 		if (S + 1 < NS)
 			step(S + 1, B, A);
 	}
+#ifdef XA_DBG_TIMES
+	{
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
+		/* HW_ID (id 4): cu 11:8, se 15:13; XCC_ID (id 20) */
+		const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+		const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+		if (lane == 0) {
+			trec[0] = t_start;
+			trec[1] = t_warm;
+			trec[2] = t_end;
+			trec[3] = (xcc & 15u) << 16 | ((hw >> 13) & 7u) << 8 |
+			    ((hw >> 8) & 15u) << 4 | ((hw >> 4) & 3u);
+		}
+	}
+#endif
 	if (NS == NW) {	/* empty chunk (never planned) */
 		gst[0] = xa_pack_state(p0[0], p1[0]);
 		gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
@@ -627,8 +674,13 @@ xa_decode_spec(xa_dec_args a)
 	typedef spec_lds2<BITS, CH, LB> L;
 	__shared__ __attribute__((aligned(16))) uint8_t
 	    lds[XA_SPEC_WPB * L::REGION];
-	spec_wave2<BITS, CH, LB, NT>(a, lds + wv * L::REGION,
-	    blockIdx.x * (64u * XA_SPEC_WPB) + wv * 64u);
+	/* every wave of the workgroup has the same chunk length unless the
+	 * balanced plan's long/short edge falls inside it */
+	const uint32_t first = blockIdx.x * (64u * XA_SPEC_WPB);
+	const bool uniform = first >= a.nlong ||
+	    first + 64u * (XA_SPEC_WPB - 1) < a.nlong;
+	spec_wave2<BITS, CH, LB, NT>(a, lds + wv * L::REGION, first + wv * 64u,
+	    uniform ? a.pace : 0u);
 }
 
 /* ------------------------------------------------------------------ */
@@ -1158,6 +1210,7 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.C = d.C;
 	a.W = b.W;
 	a.nlong = 0;
+	a.pace = 0;	/* the batch kernel decides per workgroup */
 	a.init[0] = d.init[0];
 	a.init[1] = d.init[1];
 	a.g = b.g + d.cbase;
@@ -1188,6 +1241,21 @@ xa_decode_spec_batch(xa_batch_args b)
 	    lds[XA_SPEC_WPB * batch_lds<LB>::REGION];
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const uint32_t w = blockIdx.x * XA_SPEC_WPB + wv;
+	/* lockstep (spec_wave2) only when all the workgroup's waves exist
+	 * and run the same number of super-steps: same chunk length and
+	 * channel count */
+	const uint32_t w0 = blockIdx.x * XA_SPEC_WPB;
+	bool lockstep = b.pace != 0u && w0 + XA_SPEC_WPB <= b.nwaves;
+	if (lockstep) {
+		const uint32_t s0 = b.wstream[w0];
+		const uint32_t c0 = b.streams[s0].C, f0 = b.streams[s0].fmt >> 8;
+		for (int k = 1; k < XA_SPEC_WPB; k++) {
+			const uint32_t sk = b.wstream[w0 + k];
+			lockstep = lockstep && b.streams[sk].C == c0 &&
+			    (b.streams[sk].fmt >> 8) == f0;
+		}
+	}
+	lockstep = __builtin_amdgcn_readfirstlane(lockstep);
 	if (w >= b.nwaves)
 		return;
 	const uint32_t sid = __builtin_amdgcn_readfirstlane(b.wstream[w]);
@@ -1198,7 +1266,7 @@ xa_decode_spec_batch(xa_batch_args b)
 	uint8_t *region = lds + wv * batch_lds<LB>::REGION;
 	with_format(fmt, [&](auto bc, auto cc) {
 		spec_wave2<decltype(bc)::value, decltype(cc)::value, LB, NT>(a,
-		    region, wchunk0);
+		    region, wchunk0, lockstep ? b.pace : 0u);
 	});
 }
 

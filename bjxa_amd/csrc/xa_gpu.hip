@@ -126,6 +126,29 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 	p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
 }
 
+/*
+ * Pacing of K1 (xa_dec_args::pace): for one stream, the waves of a
+ * workgroup meet at a barrier every group when a lane runs at most
+ * PACE_MAX_NS super-steps (warm-up included): there (C3: 12, C2: 11) the
+ * waves otherwise drift apart and the early finishers leave the tail to
+ * fewer requests in flight (spec -3.8 % / -3.5 %).  Batches are not paced:
+ * interleaved A/B measured no gain on C5g (NS 18), C4 and C5 (NS 130), a
+ * loss of 1-3 % with a barrier every group.  Tuning variant
+ * bits 8-11 override: 15 = off, 1-14 = barrier every that many groups.
+ */
+#define PACE_MAX_NS	32u
+
+static uint32_t
+pick_pace(uint32_t ns, bool batch, const bjxa_hip_tuning_t *t)
+{
+	const uint32_t code = t ? (t->variant >> 8) & 15u : 0u;
+	if (code == 15u)
+		return 0u;
+	if (code != 0u)
+		return code;
+	return !batch && ns <= PACE_MAX_NS ? 1u : 0u;
+}
+
 /* kernel structure (xa_decode.hip launch()): bit 1 = non-temporal PCM
  * stores, bits 2-3 = store-phase bytes per lane (measured, DESIGN.md §5:
  * stereo NT + one eblock = 128 B; mono NT + 128 B) */
@@ -210,6 +233,7 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.C = p.C;
 	a.W = p.W;
 	a.nlong = p.nlong;
+	a.pace = pick_pace((p.W + p.C) / XA_CHUNK_Q(s->channels), false, tune);
 	a.init[0] = ((uint32_t)(uint16_t)s->state[0]) |
 	    ((uint32_t)(uint16_t)s->state[1] << 16);
 	a.init[1] = ((uint32_t)(uint16_t)s->state[2]) |
@@ -455,6 +479,9 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	a.nstreams = n;
 	a.nwaves = (uint32_t)nwaves;
 	a.W = (w + 7) & ~7u;	/* a whole chunk quantum of every format */
+	/* super-steps of a lane: its channel blocks (warm-up included) over
+	 * the 8 per super-step, the same for every format */
+	a.pace = pick_pace((uint32_t)((a.W * 2u + cb) / 8u), true, tune);
 	a.g = (uint2 *)(ws + o_g);
 	a.e = (uint2 *)(ws + o_e);
 	a.queue = (uint32_t *)(ws + o_q);

@@ -46,7 +46,10 @@ typedef struct {
 					 * around the speculative-decode kernel */
 	uint32_t	variant;	/* bits 0-3: kernel structure, 0 = automatic
 					 * (DESIGN.md §3); bit 5: two-length chunk
-					 * plan.  Pass the same tuning to
+					 * plan; bits 8-11: pacing of the
+					 * speculative kernel's waves (0 = automatic,
+					 * 15 = off, n = a barrier every n groups).
+					 * Pass the same tuning to
 					 * bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 

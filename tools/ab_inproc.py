@@ -1,0 +1,149 @@
+"""In-process interleaved A/B of library builds on one GPU: every build is
+loaded side by side (ctypes, RTLD_LOCAL) and decodes the same
+device-resident stream in rotation, so box-to-box and run-to-run drift hit
+all variants alike.  Reports per build the median step time (spec + fix,
+events around bjxa_hip_decode_async), the median spec-kernel time, and
+whether its PCM equals the first build's.
+
+usage: python tools/ab_inproc.py [--wl C3|C2|C4|C5|C5g] [--mix A] [--reps 6]
+           [--steps 20] label=path[:variant[:chunk[:warmup]]] ...
+(C4/C5/C5g: the batched decode, bjxa_hip_batch_*, streams seeded as bench.py)
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+from bjxa_amd import synth, HipStream, HipTuning  # noqa: E402
+
+WL = {"C3": (5_000_000, 8, 2), "C2": (10_000_000, 8, 1), "C3s": (1_000_000, 8, 2)}
+BATCH = ("C4", "C5", "C5g")
+
+
+def load(path):
+    L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
+    L.bjxa_hip_decode_workspace.restype = ctypes.c_size_t
+    L.bjxa_hip_decode_workspace.argtypes = [ctypes.c_uint32, ctypes.c_uint, ctypes.c_void_p]
+    L.bjxa_hip_workspace_init.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    L.bjxa_hip_batch_new.restype = ctypes.c_void_p
+    L.bjxa_hip_batch_new.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_void_p]
+    L.bjxa_hip_batch_decode_async.argtypes = [ctypes.c_void_p] * 4
+    L.bjxa_hip_batch_free.argtypes = [ctypes.c_void_p]
+    L.bjxa_hip_decode_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--wl", default="C3")
+    ap.add_argument("--mix", default="A")
+    ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("builds", nargs="+")
+    args = ap.parse_args()
+    batch = args.wl in BATCH
+    if batch:
+        import bench
+        inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)))
+        srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
+        dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+                for _, _, ch, eb, _ in inputs]
+        arr = (HipStream * len(inputs))()
+        for i, ((_, bits, ch, eb, _), s_, d_) in enumerate(zip(inputs, srcs, dsts)):
+            arr[i] = HipStream(s_.data_ptr(), d_.data_ptr(), eb * 32, eb, bits, ch,
+                               (ctypes.c_int16 * 4)(0, 0, 0, 0))
+        dst = dsts[0]
+        st = torch.zeros(8 * len(inputs), dtype=torch.int32, device="cuda")
+        eb = bits = ch = 0
+    else:
+        eb, bits, ch = WL[args.wl]
+        xa = synth.stream(eb, bits, ch, args.mix, seed=0)
+        src = torch.from_numpy(xa).cuda()
+        dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(8, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                        ctypes.c_void_p]
+    builds = []
+    for spec in args.builds:
+        label, rest = spec.split("=", 1)
+        parts = rest.split(":")
+        path = parts[0]
+        var = int(parts[1], 0) if len(parts) > 1 and parts[1] else 0
+        chunk = int(parts[2]) if len(parts) > 2 and parts[2] else 0
+        warm = int(parts[3]) if len(parts) > 3 and parts[3] else -1
+        L = load(path)
+        tune = HipTuning(chunk, warm)
+        tune.variant = var
+        if batch:
+            bp = L.bjxa_hip_batch_new(arr, len(inputs), ctypes.byref(tune), sh)
+            assert bp, "batch_new failed"
+            n, ws = bp, None
+        else:
+            n = L.bjxa_hip_decode_workspace(eb, ch, ctypes.byref(tune))
+            ws = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            L.bjxa_hip_workspace_init(ws.data_ptr(), n, sh)
+        evs = []
+        for _ in range(args.steps):
+            a, b = ctypes.c_void_p(), ctypes.c_void_p()
+            hip.hipEventCreate(ctypes.byref(a))
+            hip.hipEventCreate(ctypes.byref(b))
+            evs.append((a.value, b.value))
+        builds.append({"label": label, "L": L, "tune": tune, "ws": ws, "n": n, "evs": evs,
+                       "step": [], "spec": [], "sum": None})
+    s = None if batch else HipStream(src.data_ptr(), dst.data_ptr(), eb * 32, eb, bits, ch,
+                                     (ctypes.c_int16 * 4)(0, 0, 0, 0))
+
+    def run(b, timed):
+        t = b["tune"]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(args.steps):
+            if timed:
+                t.ev_spec[0], t.ev_spec[1] = b["evs"][i]
+                e0.record()
+            if batch:
+                rc = b["L"].bjxa_hip_batch_decode_async(b["n"], st.data_ptr(),
+                                                        ctypes.byref(t), sh)
+            else:
+                rc = b["L"].bjxa_hip_decode_async(ctypes.byref(s), b["ws"].data_ptr(), b["n"],
+                                                  st.data_ptr(), ctypes.byref(t), sh)
+            assert rc == 0
+            if timed:
+                e1.record()
+                e1.synchronize()
+                b["step"].append(e0.elapsed_time(e1))
+                f = ctypes.c_float()
+                hip.hipEventElapsedTime(ctypes.byref(f), *b["evs"][i])
+                b["spec"].append(f.value)
+        t.ev_spec[0] = t.ev_spec[1] = None
+
+    for b in builds:
+        run(b, False)
+    torch.cuda.synchronize()
+    for r in range(args.reps):
+        order = builds[r % len(builds):] + builds[:r % len(builds)]
+        for b in order:
+            run(b, True)
+            if b["sum"] is None:
+                torch.cuda.synchronize()
+                b["sum"] = int(dst.view(torch.int16).to(torch.int64).sum().item()) ^ \
+                    int(dst[::4093].to(torch.int64).sum().item()) << 40
+            dst.fill_(0)
+    ref = builds[0]["sum"]
+    for b in builds:
+        print("%-10s step %.4f ms (p10 %.4f)  spec %.4f ms (p10 %.4f)  same-as-first %s" % (
+            b["label"], np.median(b["step"]), np.percentile(b["step"], 10),
+            np.median(b["spec"]), np.percentile(b["spec"], 10), b["sum"] == ref), flush=True)
+
+
+if __name__ == "__main__":
+    main()
