@@ -56,6 +56,9 @@
 #ifndef XA_SPEC_WPB
 #define XA_SPEC_WPB 4		/* waves per workgroup */
 #endif
+#ifndef XA_FIX_PF
+#define XA_FIX_PF 4		/* repair windows in flight per lane */
+#endif
 #ifndef XA_DMA_AUX
 #define XA_DMA_AUX 0		/* cache policy bits of the input LDS-DMA */
 #endif
@@ -653,13 +656,9 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 		gst[1] = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
 	}
 	if (chunk < a.nchunks) {
-		uint2 gv, ev;
-		gv.x = gst[0];
-		gv.y = gst[1];
-		ev.x = xa_pack_state(p0[0], p1[0]);
-		ev.y = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
-		a.g[chunk] = gv;
-		a.e[chunk] = ev;
+		a.g[chunk] = make_uint2(gst[0], gst[1]);
+		a.e[chunk] = make_uint2(xa_pack_state(p0[0], p1[0]),
+		    CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u);
 	}
 }
 
@@ -687,74 +686,39 @@ xa_decode_spec(xa_dec_args a)
 /* repair path                                                          */
 
 /*
- * The repair path is latency-bound (a few busy lanes per wave), and a lone
- * lane running both channels of a stereo chunk is bound by the wave's
- * instruction issue, not by the predictor's dependency chain.  So each
- * channel gets its own lane (lanes 2k, 2k+1 of a wave for stereo chunk k;
- * one instruction stream advances both), and the step uses a shorter chain:
+ * Re-decode chunk q from the state s (s.x: channel 0, s.y: channel 1),
+ * rewriting its PCM, on one lane: the eblock goes through K1's own
+ * decode_eblock (stereo: both channels in one packed-f32 instruction stream,
+ * 11 VALU per frame, with the output frame packed by the step itself; mono:
+ * the f32 chain), so repaired PCM is K1's arithmetic bit for bit.  Stops
+ * once a block-end state equals the stored trajectory (frames 30/31 of the
+ * old PCM) in every channel: nothing after it can change.  Returns true if
+ * it met the trajectory; otherwise stores the chunk's new exit state in
+ * e[q] and returns it in `exit`.
  *
- *   t + trunc(g / 256) = med3(floor(ha / 256), floor(hb / 256), t)
- *   with ha = g + 256 t, hb = ha + 255
- *
- * (floor <= trunc <= ceil and trunc is the one nearest zero, i.e. the median
- * of floor, ceil and 0; adding t and scaling by 256 commute with the median).
- * The int16 clamp folds in as med3(min(ha, HI), max(hb, LO), 256 t) with
- * LO = -32768 * 256 and HI = 32767 * 256 + 255, because 256 t already lies
- * in [LO, HI].  p1*K1 + 256 t is ready a step early, so the chain is
- * mad24, max, med3, ashr: four operations instead of seven.
- */
-__device__ __forceinline__ int32_t
-xa_med3(int32_t a, int32_t b, int32_t c)
-{
-	int32_t d;
-	asm("v_med3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-	return d;
-}
-
-__device__ __forceinline__ int32_t
-xa_step_lat(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
-    int32_t &p1)
-{
-	const int32_t t256 = (top >> sh) << 8;
-	const int32_t c = __mul24(p1, k1) + t256;
-	const int32_t ha = __mul24(p0, k0) + c;
-	const int32_t hb = __mul24(p0, k0) + (c + 255);
-	const int32_t s = xa_med3(min(ha, 32767 * 256 + 255),
-	    max(hb, -32768 * 256), t256) >> 8;
-	p1 = p0;
-	p0 = s;
-	return s;
-}
-
-/* value of the other lane of this lane's pair (lanes 2k <-> 2k+1) */
-__device__ __forceinline__ uint32_t
-pair_swap(uint32_t v)
-{
-	/* DPP quad_perm [1, 0, 3, 2] */
-	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);
-}
-
-/*
- * Re-decode channel c of chunk q from that channel's state `sc`, rewriting
- * its PCM; run by CH lanes together (the pair for stereo), which take the
- * same path.  Stops once a block-end state equals the stored trajectory's
- * in every channel (nothing after it can change).  Returns true if it met
- * the stored trajectory; otherwise returns the chunk's new exit state in
- * `exit` (both channels, every lane) and lane c == 0 stores it in e[q].
+ * The repair is one serial chain per chunk, so its time is its instruction
+ * count: the earlier lane-per-channel integer form issued ~467 VALU per
+ * repaired block (a lane pair per stereo chunk, plus the frame shuffle
+ * between them); this one ~11 per frame.
  *
  * No load sits under a branch (hipcc drains vmcnt(0) right after such
- * loads): the next block's window and old end state are fetched every
- * iteration with clamped addresses, one block ahead.
+ * loads): the windows and old end states of the blocks XA_FIX_PF ahead are
+ * fetched every iteration with clamped addresses.  BUF (one stream per
+ * launch, under 4 GiB of XA): the window comes through a buffer descriptor
+ * of the stream, whose range check returns 0 past the end, instead of
+ * per-dword 64-bit clamps.
  */
 template <int BITS, int CH, bool BUF = false>
-__device__ bool
-fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
+__device__ __forceinline__ bool
+fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 {
 	typedef geo<BITS, CH> g;
-	constexpr int BSZ = g::BSZ, EBSZ = g::EBSZ, OB = g::OB;
-	constexpr int WN = (BSZ + 3) / 4;	/* dwords of one channel block */
-	int32_t p0, p1;
-	xa_unpack_state(sc, p0, p1);
+	constexpr int EBSZ = g::EBSZ, OB = g::OB;
+	constexpr int WN = (EBSZ + 3) / 4;	/* dwords of one eblock */
+	int32_t p0[CH], p1[CH];
+	xa_unpack_state(s.x, p0[0], p1[0]);
+	if (CH == 2)
+		xa_unpack_state(s.y, p0[CH - 1], p1[CH - 1]);
 	const int64_t eblocks = a.eblocks;
 	const int64_t b0 = chunk_start<g::G2>(a, q);
 	int64_t b1 = chunk_start<g::G2>(a, q + 1);
@@ -762,12 +726,9 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 		b1 = eblocks;
 	const int64_t ndw = (eblocks * EBSZ + 3) / 4;
 	const uint32_t *src = (const uint32_t *)a.src;
+	/* q >= 1, so the stream has whole blocks (nfull >= b0 >= 16) */
+	const int64_t nfull = (int64_t)(a.pcm_bytes / OB);
 
-	uint32_t raw[WN + 1], nraw[WN + 1];
-	/* BUF (one stream per launch, under 4 GiB of XA): the window comes
-	 * through a buffer descriptor of the stream, whose range check
-	 * returns 0 past the end, so the per-dword 64-bit clamps (about 90 of
-	 * the ~530 instructions a repaired block issues) go away */
 	__amdgpu_buffer_rsrc_t rs;
 	if constexpr (BUF) {
 		const uint64_t sp = (uint64_t)a.src;
@@ -777,8 +738,9 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 		rs = __builtin_amdgcn_make_buffer_rsrc(
 		    (void *)(((uint64_t)hi << 32) | lo), 0, (int)nb, 0x00020000);
 	}
+	/* the WN + 1 dwords holding eblock b */
 	auto fetch = [&](uint32_t *r, int64_t b) {
-		const int64_t d0 = (b * EBSZ + c * BSZ) >> 2;
+		const int64_t d0 = (b * EBSZ) >> 2;
 		if constexpr (BUF) {
 			const uint32_t o = (uint32_t)d0 * 4u;
 #pragma unroll
@@ -791,102 +753,77 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 				r[i] = src[min(d0 + i, ndw - 1)];
 		}
 	};
-	/* old end state (frames 30, 31) of channel c of block b */
-	auto old_state = [&](int64_t b) -> uint32_t {
-		const uint8_t *o = a.dst + min(b, eblocks - 1) * OB;
+	/* old end state of every channel of block b (frames 30, 31), clamped
+	 * to the last whole block: a stream whose last block is cut is never
+	 * read past its PCM */
+	auto old_state = [&](int64_t b, uint32_t *o) {
+		const uint8_t *p = a.dst + min(b, nfull - 1) * OB;
 		if (CH == 2) {
-			const uint2 f = *(const uint2 *)(o + 30 * 4);
-			const uint32_t s1 = c ? f.x >> 16 : f.x & 0xffffu;
-			const uint32_t s0 = c ? f.y >> 16 : f.y & 0xffffu;
-			return s0 | (s1 << 16);
+			const uint2 f = *(const uint2 *)(p + 120);
+			o[0] = (f.y & 0xffffu) | (f.x << 16);
+			o[CH - 1] = (f.y >> 16) | (f.x & 0xffff0000u);
+		} else {
+			const uint32_t f = *(const uint32_t *)(p + 60);
+			o[0] = (f >> 16) | (f << 16);
 		}
-		const uint32_t f = *(const uint32_t *)(o + 30 * 2);
-		return (f >> 16) | (f << 16);
 	};
-	/* decode channel c of the block whose window is r; returns this
-	 * lane's 64-B share of the block's PCM in F: stereo frames
-	 * 16c..16c+15 (the other channel's samples come from the pair lane),
-	 * or the whole mono block */
-	auto decode = [&](const uint32_t *r, int64_t b, uint32_t *F) {
-		const uint32_t o = (uint32_t)(b * EBSZ + c * BSZ) & 3u;
+	auto none = [](int) {};
+	/* decode eblock b from its window r, PCM to `out` (16-B pieces) */
+	auto decode = [&](const uint32_t *r, int64_t b, uint8_t *out) {
+		const uint32_t o = (uint32_t)(b * EBSZ) & 3u;
 		uint32_t w[WN];
 #pragma unroll
 		for (int i = 0; i < WN; i++)
 			w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], o);
-		const uint32_t prof = w[0] & 0xffu;
-		const uint32_t sh = 16u + (prof & 15u);
-		int32_t k0, k1;
-		xa_gain((prof >> 4) & 7u, k0, k1);
-		/* P[j]: samples 2j, 2j+1 of this channel */
-		uint32_t P[16];
-#pragma unroll
-		for (int j = 0; j < 16; j++) {
-			const int32_t sa = xa_step_lat(code_at<BITS>(w, 0, 2 * j), sh,
-			    k0, k1, p0, p1);
-			const int32_t sb = xa_step_lat(code_at<BITS>(w, 0, 2 * j + 1),
-			    sh, k0, k1, p0, p1);
-			P[j] = __builtin_amdgcn_perm((uint32_t)sb, (uint32_t)sa,
-			    0x05040100u);
-		}
-		if (CH == 2) {
-#pragma unroll
-			for (int j = 0; j < 8; j++) {
-				const uint32_t x = c ? P[j] : P[j + 8];
-				const uint32_t y = c ? P[j + 8] : P[j];
-				const uint32_t rv = pair_swap(x);
-				const uint32_t lp = c ? rv : y, rp = c ? y : rv;
-				F[2 * j] = __builtin_amdgcn_perm(rp, lp, 0x05040100u);
-				F[2 * j + 1] = __builtin_amdgcn_perm(rp, lp,
-				    0x07060302u);
-			}
-		} else {
-#pragma unroll
-			for (int j = 0; j < 16; j++)
-				F[j] = P[j];
-		}
+		(void)decode_eblock<BITS, CH, true, false, OB>(w, 0, p0, p1, out,
+		    none);
 	};
-	/* whole blocks in the loop (always four 16-B stores, so the wait
-	 * for the prefetched window can leave them in flight); the stream's
-	 * cut last block, if it is this chunk's, after it */
-	const int64_t nfull = (int64_t)(a.pcm_bytes / OB);
+
+	constexpr int PF = XA_FIX_PF;
 	const int64_t bf = min(b1, nfull);
-	fetch(raw, b0);
-	uint32_t old = old_state(b0);
+	uint32_t ring[PF][WN + 1], rold[PF][CH];
+#pragma unroll
+	for (int j = 0; j < PF; j++) {
+		fetch(ring[j], b0 + j);
+		old_state(b0 + j, rold[j]);
+	}
 	bool met = false;
 	int64_t b = b0;
-	for (; b < bf; b++) {
-		fetch(nraw, b + 1);
-		const uint32_t nold = old_state(b + 1);
-		uint32_t F[16];
-		decode(raw, b, F);
-		u32x4a *d = (u32x4a *)(a.dst + (uint64_t)b * OB + (uint64_t)c * 64u);
+	while (b < bf) {
+		bool stop = false;
 #pragma unroll
-		for (int i = 0; i < 4; i++) {
-			u32x4a v = { F[4 * i], F[4 * i + 1], F[4 * i + 2],
-			    F[4 * i + 3] };
-			d[i] = v;
-		}
-		if (b + 1 < eblocks) {
-			uint32_t m = xa_pack_state(p0, p1) == old;
-			if (CH == 2)
-				m &= pair_swap(m);
+		for (int j = 0; j < PF; j++) {
+			if (stop)
+				break;
+			decode(ring[j], b, a.dst + (uint64_t)b * OB);
+			bool m = b + 1 < eblocks;
+#pragma unroll
+			for (int c = 0; c < CH; c++)
+				m = m && xa_pack_state(p0[c], p1[c]) == rold[j][c];
+			/* refill before the exits: no load under a branch */
+			fetch(ring[j], b + PF);
+			old_state(b + PF, rold[j]);
+			b++;
 			if (m) {
 				met = true;
-				break;
+				stop = true;
+			} else if (b >= bf) {
+				stop = true;
 			}
 		}
-#pragma unroll
-		for (int i = 0; i <= WN; i++)
-			raw[i] = nraw[i];
-		old = nold;
+		if (stop)
+			break;
 	}
 	if (!met && b < b1) {
 		/* b == eblocks - 1, PCM cut short: no later block to meet */
-		uint32_t F[16];
-		decode(raw, b, F);
-		const uint64_t off = (uint64_t)b * OB + (uint64_t)c * 64u;
+		uint32_t raw[WN + 1];
+		uint32_t F[OB / 4] __attribute__((aligned(16)));
+		fetch(raw, b);
+		decode(raw, b, (uint8_t *)F);
+		const uint64_t off = (uint64_t)b * OB;
 		uint8_t *d = a.dst + off;
-		for (int k = 0; k < 16; k++) {
+#pragma unroll
+		for (int k = 0; k < OB / 4; k++) {
 			if (off + 4u * k + 4u <= a.pcm_bytes)
 				((uint32_t *)d)[k] = F[k];
 			else if (off + 4u * k < a.pcm_bytes)
@@ -895,17 +832,9 @@ fix_lane(const xa_dec_args &a, uint32_t q, int c, uint32_t sc, uint2 &exit)
 	}
 	if (met)
 		return true;
-	const uint32_t st = xa_pack_state(p0, p1);
-	if (CH == 2) {
-		const uint32_t other = pair_swap(st);
-		exit.x = c ? other : st;
-		exit.y = c ? st : other;
-	} else {
-		exit.x = st;
-		exit.y = 0u;
-	}
-	if (c == 0)
-		a.e[q] = exit;
+	exit.x = xa_pack_state(p0[0], p1[0]);
+	exit.y = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
+	a.e[q] = exit;
 	return false;
 }
 
@@ -946,43 +875,31 @@ heap_pop(uint32_t *h, uint32_t &n)
 }
 
 /*
- * The sequential tail (the first CH lanes of one wave: repairs run a lane
- * per channel; the heap lives in lane 0): drain the re-check queue in chunk
+ * The sequential tail (lane 0 of one wave): drain the re-check queue in chunk
  * order (a heap, so even a pathological cascade costs O(n log n)
  * bookkeeping), then publish the status words and reset the control words.
  * Queue entries are >= 1, so 0 ends the loop.
  */
 template <int BITS, int CH, bool BUF>
-__device__ void
+__device__ __forceinline__ void
 drain_tail(const xa_dec_args &a)
 {
-	const int c = threadIdx.x;
 	const uint32_t nq = a.ctl[XA_CTL_NQ];
 	uint32_t n = 0, tail = 0;
-	if (c == 0)
-		for (uint32_t i = 0; i < nq; i++)
-			heap_push(a.queue, n, a.queue[i]);
-	for (;;) {
-		uint32_t q = 0;
-		if (c == 0 && n > 0)
-			q = heap_pop(a.queue, n);
-		q = __builtin_amdgcn_readfirstlane(q);
-		if (q == 0)
-			break;
+	for (uint32_t i = 0; i < nq; i++)
+		heap_push(a.queue, n, a.queue[i]);
+	while (n > 0) {
+		const uint32_t q = heap_pop(a.queue, n);
 		const uint2 s = a.e[q - 1], gq = a.g[q];
 		if (s.x == gq.x && s.y == gq.y)
 			continue;
 		tail++;
 		uint2 ex;
-		const bool met = fix_lane<BITS, CH, BUF>(a, q, c, c ? s.y : s.x, ex);
-		if (c == 0) {
-			a.g[q] = s;
-			if (!met && q + 1 < a.nchunks)
-				heap_push(a.queue, n, q + 1);
-		}
+		const bool met = fix_chunk<BITS, CH, BUF>(a, q, s, ex);
+		a.g[q] = s;
+		if (!met && q + 1 < a.nchunks)
+			heap_push(a.queue, n, q + 1);
 	}
-	if (c != 0)
-		return;
 	const uint2 fin = a.e[a.nchunks - 1];
 	a.status[XA_ST_ERR] = a.ctl[XA_CTL_ERR];
 	a.status[XA_ST_STATE_L] = fin.x;
@@ -1012,6 +929,21 @@ drain_tail(const xa_dec_args &a)
 #ifndef XA_FIX_CPT
 #define XA_FIX_CPT 2
 #endif
+#ifndef XA_FIX_REL
+#define XA_FIX_REL 0
+#endif
+
+/* K2's release before the arrival ticket */
+__device__ __forceinline__ void
+xa_fix_release()
+{
+#if XA_FIX_REL == 1
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
+	__threadfence();
+#endif
+}
+
 
 template <int BITS, int CH, bool BUF>
 __global__ __launch_bounds__(256) void
@@ -1054,17 +986,13 @@ xa_decode_fix(xa_dec_args a)
 		}
 		__syncthreads();
 		const uint32_t nf = nfix;
-		/* a lane per channel: stereo chunk k on lanes 2k, 2k+1 */
-		const int c = threadIdx.x % CH;
-		for (uint32_t k = threadIdx.x / CH; k < nf; k += 256u / CH) {
+		/* a lane per listed chunk */
+		for (uint32_t k = threadIdx.x; k < nf; k += 256u) {
 			const uint32_t q = fixq[k];
 			const uint2 s = fixs[k];
 			uint2 ex;
-			const bool met = fix_lane<BITS, CH, BUF>(a, q, c, c ? s.y : s.x,
-			    ex);
+			const bool met = fix_chunk<BITS, CH, BUF>(a, q, s, ex);
 			wrote = true;
-			if (c != 0)
-				continue;
 			a.g[q] = s;
 			if (!met && q + 1 < n) {
 				uint32_t i = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
@@ -1083,13 +1011,13 @@ xa_decode_fix(xa_dec_args a)
 	const int any = __syncthreads_or(wrote);
 	if (threadIdx.x == 0) {
 		if (any) {
-			__threadfence();
+			xa_fix_release();
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		}
 		last = atomicAdd(&a.ctl[XA_CTL_TICKET], 1u) == gridDim.x - 1;
 	}
 	__syncthreads();
-	if (!last || threadIdx.x >= CH)
+	if (!last || threadIdx.x != 0)
 		return;
 	/* acquire: this CU now sees every other workgroup's writes */
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1270,48 +1198,53 @@ xa_decode_spec_batch(xa_batch_args b)
 	});
 }
 
+/* fix_chunk in a stream's format (a per-lane switch: no generic lambda, so
+ * the argument block stays in registers) */
+__device__ __forceinline__ bool
+fix_any(const xa_dec_args &a, uint32_t fmt, uint32_t q, uint2 s, uint2 &ex)
+{
+	switch (fmt) {
+	case 8 | 2 << 8:
+		return fix_chunk<8, 2>(a, q, s, ex);
+	case 6 | 2 << 8:
+		return fix_chunk<6, 2>(a, q, s, ex);
+	case 4 | 2 << 8:
+		return fix_chunk<4, 2>(a, q, s, ex);
+	case 8 | 1 << 8:
+		return fix_chunk<8, 1>(a, q, s, ex);
+	case 6 | 1 << 8:
+		return fix_chunk<6, 1>(a, q, s, ex);
+	default:
+		return fix_chunk<4, 1>(a, q, s, ex);
+	}
+}
+
 /*
- * Sequential tail of a batch (lanes 0 and 1 of one wave; the heap lives in
- * lane 0): drain the re-check queue in global chunk order.  Global chunk
+ * Sequential tail of a batch (lane 0 of one wave): drain the re-check queue
+ * in global chunk order.  Global chunk
  * indices never cross streams (a stream's chunk 0 is never queued).
  */
-__device__ static void
+__device__ __forceinline__ void
 drain_batch(const xa_batch_args &b)
 {
-	const int c = threadIdx.x;
 	const uint32_t nq = b.ctl[XA_CTL_NQ];
 	uint32_t n = 0;
-	if (c == 0)
-		for (uint32_t i = 0; i < nq; i++)
-			heap_push(b.queue, n, b.queue[i]);
-	for (;;) {
-		uint32_t Q = 0;
-		if (c == 0 && n > 0)
-			Q = heap_pop(b.queue, n);
-		Q = __builtin_amdgcn_readfirstlane(Q);
-		if (Q == 0)
-			break;
+	for (uint32_t i = 0; i < nq; i++)
+		heap_push(b.queue, n, b.queue[i]);
+	while (n > 0) {
+		const uint32_t Q = heap_pop(b.queue, n);
 		const uint2 s = b.e[Q - 1], gq = b.g[Q];
 		if (s.x == gq.x && s.y == gq.y)
 			continue;
 		const uint32_t sid = b.wstream[Q / 64];
 		const xa_dec_args a = batch_stream_args(b, sid);
 		const uint32_t q = Q - b.streams[sid].cbase;
-		const uint32_t fmt = b.streams[sid].fmt;
-		bool met = false;
-		if (c == 0 || (fmt >> 8) == 2) {
-			uint2 ex;
-			with_format(fmt, [&](auto bc, auto cc) {
-				met = fix_lane<decltype(bc)::value,
-				    decltype(cc)::value>(a, q, c, c ? s.y : s.x, ex);
-			});
-		}
-		if (c == 0) {
-			b.g[Q] = s;
-			b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_TAIL]++;
-			if (!met && q + 1 < a.nchunks)
-				heap_push(b.queue, n, Q + 1);
-		}
+		uint2 ex;
+		const bool met = fix_any(a, b.streams[sid].fmt, q, s, ex);
+		b.g[Q] = s;
+		b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_TAIL]++;
+		if (!met && q + 1 < a.nchunks)
+			heap_push(b.queue, n, Q + 1);
 	}
 }
 
@@ -1358,26 +1291,16 @@ xa_decode_fix_batch(xa_batch_args b)
 		}
 		__syncthreads();
 		const uint32_t nf = nfix;
-		/* a lane pair per chunk (the second idles on mono streams) */
-		const int c = threadIdx.x & 1;
-		for (uint32_t k = threadIdx.x / 2; k < nf; k += 128u) {
+		/* a lane per listed chunk */
+		for (uint32_t k = threadIdx.x; k < nf; k += 256u) {
 			const uint32_t Q = fixq[k];
 			const uint2 s = fixs[k];
 			const uint32_t sid = b.wstream[Q / 64];
 			const xa_dec_args a = batch_stream_args(b, sid);
 			const uint32_t q = Q - b.streams[sid].cbase;
-			const uint32_t fmt = b.streams[sid].fmt;
-			if (c == 1 && (fmt >> 8) == 1)
-				continue;
-			bool met = false;
 			uint2 ex;
-			with_format(fmt, [&](auto bc, auto cc) {
-				met = fix_lane<decltype(bc)::value,
-				    decltype(cc)::value>(a, q, c, c ? s.y : s.x, ex);
-			});
+			const bool met = fix_any(a, b.streams[sid].fmt, q, s, ex);
 			wrote = true;
-			if (c != 0)
-				continue;
 			b.g[Q] = s;
 			atomicAdd(&b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_FIXED], 1u);
 			if (!met && q + 1 < a.nchunks) {
@@ -1392,7 +1315,7 @@ xa_decode_fix_batch(xa_batch_args b)
 	const int any = __syncthreads_or(wrote);
 	if (threadIdx.x == 0) {
 		if (any) {
-			__threadfence();
+			xa_fix_release();
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		}
 		last = atomicAdd(&b.ctl[XA_CTL_TICKET], 1u) == gridDim.x - 1;
@@ -1402,7 +1325,7 @@ xa_decode_fix_batch(xa_batch_args b)
 		return;
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	if (threadIdx.x < 2)
+	if (threadIdx.x == 0)
 		drain_batch(b);
 	__syncthreads();
 	for (uint32_t sid = threadIdx.x; sid < b.nstreams; sid += 256u) {

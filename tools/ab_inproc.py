@@ -6,7 +6,7 @@ events around bjxa_hip_decode_async), the median spec-kernel time, and
 whether its PCM equals the first build's.
 
 usage: python tools/ab_inproc.py [--wl C3|C2|C4|C5|C5g] [--mix A] [--reps 6]
-           [--steps 20] label=path[:variant[:chunk[:warmup]]] ...
+           [--steps 20] [--layout sep|packed] label=path[:variant[:chunk[:warmup]]] ...
 (C4/C5/C5g: the batched decode, bjxa_hip_batch_*, streams seeded as bench.py)
 """
 import argparse
@@ -21,7 +21,8 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, ROOT)
 from bjxa_amd import synth, HipStream, HipTuning  # noqa: E402
 
-WL = {"C3": (5_000_000, 8, 2), "C2": (10_000_000, 8, 1), "C3s": (1_000_000, 8, 2)}
+WL = {"C3": (5_000_000, 8, 2), "C2": (10_000_000, 8, 1), "C3s": (1_000_000, 8, 2),
+      "C5s": (128 * 65536, 8, 2)}   # C5g's eblocks as one stream
 BATCH = ("C4", "C5", "C5g")
 
 
@@ -46,15 +47,46 @@ def main():
     ap.add_argument("--mix", default="A")
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--eblocks", type=int, default=0,
+                    help="single-stream workloads: override the stream length")
+    ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps"],
+                    help="batches: one allocation per stream buffer (sep) or all "
+                         "streams back to back in one allocation (packed)")
     ap.add_argument("builds", nargs="+")
     args = ap.parse_args()
-    batch = args.wl in BATCH
+    batch = args.wl in BATCH or args.wl.startswith("C3x")
     if batch:
         import bench
-        inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)))
-        srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
-        dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
-                for _, _, ch, eb, _ in inputs]
+        if args.wl.startswith("C3x"):
+            # C3's 5M eblocks as n separately allocated streams (C3x<n>)
+            n = int(args.wl[3:])
+            inputs = [(i, 8, 2, 5_000_000 // n, synth.stream(5_000_000 // n, 8, 2, "A",
+                                                            seed=1000 + i))
+                      for i in range(n)]
+        else:
+            inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)))
+        if args.layout in ("packed", "gaps"):
+            # every stream in one allocation, back to back at 256-B steps
+            # (gaps: plus a seeded random gap of 0-255 x 256 B before each)
+            rng = np.random.default_rng(7)
+
+            def carve(sizes):
+                offs, o = [], 0
+                for n in sizes:
+                    if args.layout == "gaps":
+                        o += int(rng.integers(0, 256)) * 256
+                    offs.append(o)
+                    o += (n + 255) // 256 * 256
+                big = torch.empty(o, dtype=torch.uint8, device="cuda")
+                return [big[a:a + n] for a, n in zip(offs, sizes)]
+            srcs = carve([x.size for *_, x in inputs])
+            for t_, (*_, x) in zip(srcs, inputs):
+                t_.copy_(torch.from_numpy(x))
+            dsts = carve([eb * 64 * ch for _, _, ch, eb, _ in inputs])
+        else:
+            srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
+            dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+                    for _, _, ch, eb, _ in inputs]
         arr = (HipStream * len(inputs))()
         for i, ((_, bits, ch, eb, _), s_, d_) in enumerate(zip(inputs, srcs, dsts)):
             arr[i] = HipStream(s_.data_ptr(), d_.data_ptr(), eb * 32, eb, bits, ch,
@@ -64,6 +96,7 @@ def main():
         eb = bits = ch = 0
     else:
         eb, bits, ch = WL[args.wl]
+        eb = args.eblocks or eb
         xa = synth.stream(eb, bits, ch, args.mix, seed=0)
         src = torch.from_numpy(xa).cuda()
         dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")

@@ -1,10 +1,14 @@
 set -o pipefail
 mkdir -p gpurun_out
+R=$PWD
 L=bjxa_amd/libbjxa.so.0
-B="off=$L:0xf00 g1=$L:0x100 g2=$L:0x200 g4=$L:0x400 g8=$L:0x800"
-for wl in C3 C2 C5g C4; do
-timeout -k 10 300 python tools/ab_inproc.py --wl $wl --reps 6 --steps 20 $B > gpurun_out/ab4_$wl.log 2>&1
-echo == $wl; grep -v amdgpu.ids gpurun_out/ab4_$wl.log
+B="base=dbg/base.so:0 new=$L:0 rel=dbg/rel.so:0"
+for mx in A W F; do
+timeout -k 10 300 python tools/ab_inproc.py --wl C3 --mix $mx --reps 4 --steps 20 $B > gpurun_out/e11_C3$mx.log 2>&1
+echo == C3$mx; grep -v amdgpu.ids gpurun_out/e11_C3$mx.log
 done
-timeout -k 10 300 python tools/ab_inproc.py --wl C5 --reps 4 --steps 10 $B > gpurun_out/ab4_C5.log 2>&1
-echo == C5; grep -v amdgpu.ids gpurun_out/ab4_C5.log
+export TMPDIR=/tmp
+for mx in Z A W; do
+( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/e11_tr$mx -o run -- python3 $R/bench.py --mix $mx --no-other --no-cpu --no-verify --steps 50 > $R/gpurun_out/e11_tr$mx.log 2>&1 )
+echo == trace $mx; grep -h "xa_decode" gpurun_out/e11_tr$mx/*kernel_stats.csv | cut -d, -f1-4
+done
