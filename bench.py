@@ -37,11 +37,12 @@ Reported:
               against 8 TB/s; the read-only fraction beside it; traffic =
               HBM bytes per launch from the committed rocprofv3 PMC summary
               (profiles/pmc_latest.json) when it was taken on this workload
-  cpu_baseline  rank 0 at N = 1: the oracle (CPU restatement of libbjxa's
-              decode): C2/C3 on 1 thread (the stream is serial), C4/C5 on
-              all host cores the process may use (capped at 16, the box's
-              share), one decoder per thread, streams round-robin; median of
-              5 passes after a discarded first
+  cpu_baseline  rank 0 at N = 1, for every line: the oracle (CPU
+              restatement of libbjxa's decode/encode): C2/C3 and the encode on
+              1 thread (a stream is serial), C4/C5/C5g on all host cores the
+              process may use (capped at 16, the box's share), one decoder
+              per thread, streams round-robin; median of 5 passes after a
+              discarded first
 
 CPU rehearsal: BJXA_BENCH_BACKEND=gloo runs the N > 1 path on CPU (gloo,
 small job via --streams/--eblocks), decoding each rank's share with the
@@ -356,6 +357,12 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
     specs = batch_specs(name, nstreams, eblocks)
     lo, hi = shard_range(len(specs), rank, world)
     inputs = batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream)
+    # every stream in allocations of its own, as separate callers' buffers
+    # are: without this the allocator carves them back to back out of the
+    # previous config's cached segments, and same-size streams packed at
+    # power-of-two spacing decode up to 30 % slower ("Stream
+    # placement")
+    torch.cuda.empty_cache()
     srcs, dsts, streams = [], [], []
     samples = alg = 0
     for i, bits, ch, eb, xa in inputs:
@@ -430,7 +437,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             "first_error": first_err, "cpu_baseline": cpu}
 
 
-def run_encode(steps, warmup, dev, verify):
+def run_encode(steps, warmup, dev, verify, cpu_leg=False):
     """bjxa_hip_encode_async on C3-shaped PCM (5,000,000 8-bit stereo
     eblocks = 320M samples), the GPU side of bjxa_encode()."""
     import torch
@@ -462,17 +469,32 @@ def run_encode(steps, warmup, dev, verify):
         e1.synchronize()
         ms.append(e0.elapsed_time(e1))
     med = float(np.median(ms))
-    ok = None
-    if verify:
+    ok, cpu = None, None
+    if verify or cpu_leg:
         import oracle
-        ok = bool(np.array_equal(dst.cpu().numpy(), oracle.encode(pcm, frames, bits, ch)))
+        ref = oracle.encode(pcm, frames, bits, ch)      # also the discarded pass
+        ok = bool(np.array_equal(dst.cpu().numpy(), ref))
+        if cpu_leg:
+            times = []
+            for _ in range(CPU_PASSES):
+                t = time.perf_counter()
+                oracle.encode(pcm, frames, bits, ch)
+                times.append(time.perf_counter() - t)
+            med = float(np.median(times))
+            cpu = {"value": round(frames * ch / med / 1e6, 1), "unit": "MSamples/s",
+                   "cores": 1, "kind": "port",
+                   "sample": "the full C3-shaped PCM (%d samples), oracle/xa_oracle.c "
+                             "single-pass encode on 1 thread, median of %d passes after a "
+                             "discarded first; host CPU: %s" % (frames * ch, CPU_PASSES,
+                                                                  host_cpu())}
+        del ref
     alg = pcm.nbytes + nxa
     return {"workload": "encode, C3-shaped: 320M int16 samples (8-bit stereo) -> XA",
             "value": round(frames * ch / dt / 1e6, 1), "unit": "MSamples/s",
             "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(med, 4),
             "kernel_samples": len(ms),
             "frac": round(alg / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
-            "byte_exact": ok}
+            "byte_exact": ok, "cpu_baseline": cpu}
 
 
 def pmc_traffic(workload, mix):
@@ -575,14 +597,14 @@ def main_stream(args, workload, dev, world, rank):
             ok = ok if o["ok"] in (None, True) else False
         for name in sorted(BATCHES):
             o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify,
-                          cpu_leg=cpu_leg and name in ("C4", "C5"))
+                          cpu_leg=cpu_leg)
             for k in ("checksums", "ref_checksums", "shard"):
                 o.pop(k)
             if o["first_error"] == FIRST_ERR_NONE:
                 o["first_error"] = None
             other[name] = o
             ok = ok if o["bit_exact"] in (None, True) else False
-        o = run_encode(args.steps, args.warmup, dev, not args.no_verify)
+        o = run_encode(args.steps, args.warmup, dev, not args.no_verify, cpu_leg)
         other["encode_C3"] = o
         ok = ok if o["byte_exact"] in (None, True) else False
 

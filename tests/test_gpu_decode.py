@@ -195,3 +195,38 @@ def test_f32_rounding_regime(built, ch):
     ref, _, _, _ = oracle.decode(xa, eb, 8, ch)
     assert _big_gain_steps(xa, eb, 8, ch, ref) > 10000
     assert np.array_equal(dev_decode(xa, eb, 8, ch), ref)
+
+
+@pytest.mark.parametrize("bits", [4, 6, 8])
+@pytest.mark.parametrize("ch", [1, 2])
+def test_repair_cut_block_exact_dst(built, bits, ch):
+    """Repairs everywhere (warm-up 0, 16-eblock chunks, mix W) on a stream
+    whose last block is cut, decoded into a PCM buffer of exactly the
+    emitted frames (rounded up to the 16-B alignment) followed by a guard:
+    the repair path must emit the cut block exactly and never touch the
+    guard (the old end state of the cut block is not read)."""
+    torch = pytest.importorskip("torch")
+    eb = 4099
+    for cut in (1, 17, 31):
+        frames = eb * 32 - cut
+        xa = synth.stream(eb, bits, ch, "W", seed=bits * 7 + ch + cut)
+        ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, (9, -9, 99, -99), frames=frames)
+        nbytes = frames * 2 * ch
+        alloc = (nbytes + 15) // 16 * 16
+        buf = torch.full((alloc + 4096,), 0x5A, dtype=torch.uint8, device="cuda")
+        src = torch.from_numpy(xa).cuda()
+        ws_len = bjxa_amd.decode_workspace_size(eb, ch, 16, 0)
+        ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
+        status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        bjxa_amd.workspace_init(ws.data_ptr(), ws_len, s)
+        bjxa_amd.decode_device(src.data_ptr(), buf.data_ptr(), eb, frames, bits, ch,
+                               ws.data_ptr(), ws_len, status.data_ptr(), (9, -9, 99, -99),
+                               16, 0, s)
+        torch.cuda.synchronize()
+        out = buf.cpu().numpy()
+        st = status.cpu().numpy().view(np.uint32)
+        assert st[3] > 0                                    # repairs ran
+        assert np.array_equal(out[:nbytes].view(np.int16), ref), cut
+        assert (out[nbytes:] == 0x5A).all(), cut
+        assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
