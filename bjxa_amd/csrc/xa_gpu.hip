@@ -131,12 +131,14 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
  * workgroup meet at a barrier every group when a lane runs at most
  * PACE_MAX_NS super-steps (warm-up included): there (C3: 12, C2: 11) the
  * waves otherwise drift apart and the early finishers leave the tail to
- * fewer requests in flight (spec -3.8 % / -3.5 %).  Batches are not paced:
- * interleaved A/B measured no gain on C5g (NS 18), C4 and C5 (NS 130), a
- * loss of 1-3 % with a barrier every group.  Tuning variant
+ * fewer requests in flight (spec -3.8 % / -3.5 %).  Batches only up to
+ * PACE_MAX_NS_BATCH: C3's 5M eblocks as 16 or 64 streams (NS 11-12) gain
+ * 4.5 % / 1.1 % paced, while C5g (NS 18), C4 (NS 26) and C5 (NS 130) gain
+ * nothing or lose 1-3 % (interleaved A/B).  Tuning variant
  * bits 8-11 override: 15 = off, 1-14 = barrier every that many groups.
  */
 #define PACE_MAX_NS	32u
+#define PACE_MAX_NS_BATCH	12u
 
 static uint32_t
 pick_pace(uint32_t ns, bool batch, const bjxa_hip_tuning_t *t)
@@ -146,7 +148,7 @@ pick_pace(uint32_t ns, bool batch, const bjxa_hip_tuning_t *t)
 		return 0u;
 	if (code != 0u)
 		return code;
-	return !batch && ns <= PACE_MAX_NS ? 1u : 0u;
+	return ns <= (batch ? PACE_MAX_NS_BATCH : PACE_MAX_NS) ? 1u : 0u;
 }
 
 /* kernel structure (xa_decode.hip launch()): bit 1 = non-temporal PCM

@@ -1,5 +1,6 @@
-"""GPU encode parity: byte-exact XA against the oracle and the survey's
-reference-encoder SHA-1s; the reference's round-trip tolerance."""
+"""GPU encode parity: byte-exact XA against the oracle, the round-trip
+identity that pins the reference's encode, and the survey's
+encoder SHA-1s as a regression check."""
 import hashlib
 
 import numpy as np
@@ -30,12 +31,18 @@ def test_encode_random(built, bits, ch, frames):
 
 
 @pytest.mark.parametrize("bits", [4, 6, 8])
-def test_round_trip(built, bits):
-    """decode(encode(x)) == x with the low 16-bits bits cleared."""
+@pytest.mark.parametrize("ch", [1, 2])
+def test_round_trip(built, bits, ch):
+    """The reference's encode pins itself: every profile byte is 0
+    (src/libbjxa.c:679) and each code is the top `bits` bits of its sample
+    (:349-391), so decode(encode(x)) == x with the low 16-bits bits cleared,
+    exactly -- an identity that fixes every code byte."""
     frames = 300001
-    pcm = synth.pcm(frames, 2, seed=bits)
-    xa = dev_encode(pcm, frames, bits, 2)
-    back = dev_decode(xa, (frames + 31) // 32, bits, 2, frames=frames)
+    pcm = synth.pcm(frames, ch, seed=bits + ch)
+    xa = dev_encode(pcm, frames, bits, ch)
+    eb = (frames + 31) // 32
+    assert (xa.reshape(eb * ch, bits * 4 + 1)[:, 0] == 0).all()
+    back = dev_decode(xa, eb, bits, ch, frames=frames)
     assert np.array_equal(back, pcm & np.int16(~((1 << (16 - bits)) - 1)))
 
 
