@@ -294,7 +294,7 @@ def shard_range(n, rank, world):
     return rank * n // world, (rank + 1) * n // world
 
 
-def batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream=-1):
+def batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream=-1, mix="A"):
     """Seeded XA of streams lo..hi-1 of a batch job (seed = 1000 + global
     index, so the job is the same at every N); `bad_stream` gets a gain-5
     profile in its middle eblock (first-error collective test)."""
@@ -303,7 +303,7 @@ def batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream=-1):
     out = []
     for i in range(lo, hi):
         bits, ch, eb = specs[i]
-        xa = synth.stream(eb, bits, ch, "A", seed=1000 + i)
+        xa = synth.stream(eb, bits, ch, mix, seed=1000 + i)
         if i == bad_stream:
             xa[(eb // 2) * ch * (bits * 4 + 1)] = 0x57
         out.append((i, bits, ch, eb, xa))

@@ -1248,67 +1248,78 @@ drain_batch(const xa_batch_args &b)
 	}
 }
 
-/* K2 over a batch: as xa_decode_fix, over the global chunk space; the last
- * workgroup also publishes every stream's status */
+/*
+ * fix_chunk for one stream of a batch, wave-uniform: the format switch does
+ * not diverge, and a stream under 4 GiB of XA reads its repair windows
+ * through a buffer descriptor (the descriptor must be uniform, so this
+ * needs every lane of the wave on the same stream)
+ */
+__device__ __forceinline__ bool
+fix_uniform(const xa_dec_args &a, uint32_t fmt, uint32_t q, uint2 s, uint2 &ex)
+{
+	const bool buf = (uint64_t)a.eblocks * ((fmt & 0xffu) * 4u + 1u) *
+	    (fmt >> 8) < (1ull << 32) - 256u;
+	bool met = false;
+	with_format(fmt, [&](auto bc, auto cc) {
+		constexpr int B = decltype(bc)::value, C = decltype(cc)::value;
+		met = buf ? fix_chunk<B, C, true>(a, q, s, ex) :
+		    fix_chunk<B, C, false>(a, q, s, ex);
+	});
+	return met;
+}
+
+/*
+ * K2 over a batch.  Global wave g's 64 chunks all belong to stream
+ * wstream[g], so a wave takes one global wave at a time: lane l checks
+ * chunk 64g + l against its predecessor and, if they differ, repairs it in
+ * place.  The stream's descriptor is wave-uniform (scalar loads), so is its
+ * format, and the repair windows come through a buffer descriptor -- the
+ * first version listed the mismatches of 512 chunks in LDS and gave them
+ * to lanes in any order, so a wave mixed streams and formats: per-lane
+ * descriptor loads, every format's path run in turn, clamped pointers
+ * (C4 47 us, C5g 29 us against 18 us for one C3 stream).  The last
+ * workgroup (arrival ticket) drains the cascades and publishes every
+ * stream's status.
+ */
 __global__ __launch_bounds__(256) void
 xa_decode_fix_batch(xa_batch_args b)
 {
-	constexpr uint32_t SPAN = 256u * XA_FIX_CPT;
-	__shared__ uint32_t last, nfix;
-	__shared__ uint32_t fixq[SPAN];
-	__shared__ uint2 fixs[SPAN];
-	const uint32_t n = 64u * b.nwaves;
+	__shared__ uint32_t last;
+	const int lane = threadIdx.x & 63;
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const uint64_t *e64 = (const uint64_t *)b.e;
 	const uint64_t *g64 = (const uint64_t *)b.g;
 	bool wrote = false;
-	for (uint32_t base = blockIdx.x * SPAN; base < n;
-	    base += gridDim.x * SPAN) {
-		if (threadIdx.x == 0)
-			nfix = 0;
-		__syncthreads();
-		const uint32_t t0 = base + threadIdx.x * XA_FIX_CPT;
-		uint64_t ev[XA_FIX_CPT], gv[XA_FIX_CPT];
-#pragma unroll
-		for (int i = 0; i < XA_FIX_CPT; i++) {
-			const uint32_t Q = min(t0 + i, n - 1);
-			ev[i] = __hip_atomic_load(&e64[Q > 0 ? Q - 1 : 0],
-			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			gv[i] = g64[Q];
-		}
-#pragma unroll
-		for (int i = 0; i < XA_FIX_CPT; i++) {
-			const uint32_t Q = t0 + i;
-			if (Q >= n || ev[i] == gv[i])
-				continue;
-			const xa_batch_stream &d = b.streams[b.wstream[Q / 64]];
-			const uint32_t q = Q - d.cbase;
-			if (q > 0 && q < d.nchunks) {
-				const uint32_t k = atomicAdd(&nfix, 1u);
-				fixq[k] = Q;
-				fixs[k] = make_uint2((uint32_t)ev[i],
-				    (uint32_t)(ev[i] >> 32));
-			}
-		}
-		__syncthreads();
-		const uint32_t nf = nfix;
-		/* a lane per listed chunk */
-		for (uint32_t k = threadIdx.x; k < nf; k += 256u) {
-			const uint32_t Q = fixq[k];
-			const uint2 s = fixs[k];
-			const uint32_t sid = b.wstream[Q / 64];
-			const xa_dec_args a = batch_stream_args(b, sid);
-			const uint32_t q = Q - b.streams[sid].cbase;
+	for (uint32_t gw = blockIdx.x * 4u + wv; gw < b.nwaves; gw += gridDim.x * 4u) {
+		const uint32_t sid = __builtin_amdgcn_readfirstlane(b.wstream[gw]);
+		const xa_dec_args a = batch_stream_args(b, sid);
+		const uint32_t cbase = __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
+		const uint32_t fmt = __builtin_amdgcn_readfirstlane(b.streams[sid].fmt);
+		const uint32_t Q = 64u * gw + (uint32_t)lane, q = Q - cbase;
+		/* a stream's chunk 0 and the padding slots past its last chunk
+		 * are never checked; e[Q-1] is read whatever q is (no load
+		 * under a branch) */
+		const uint64_t ev = __hip_atomic_load(&e64[Q > 0 ? Q - 1 : 0],
+		    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const uint64_t gv = g64[Q];
+		const bool mism = q > 0 && q < a.nchunks && ev != gv;
+		const uint64_t bal = __ballot(mism);
+		if (bal == 0)
+			continue;
+		wrote = true;
+		if (lane == 0)
+			atomicAdd(&b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_FIXED],
+			    (uint32_t)__builtin_popcountll(bal));
+		if (mism) {
+			const uint2 s = make_uint2((uint32_t)ev, (uint32_t)(ev >> 32));
 			uint2 ex;
-			const bool met = fix_any(a, b.streams[sid].fmt, q, s, ex);
-			wrote = true;
+			const bool met = fix_uniform(a, fmt, q, s, ex);
 			b.g[Q] = s;
-			atomicAdd(&b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_FIXED], 1u);
 			if (!met && q + 1 < a.nchunks) {
 				uint32_t i = atomicAdd(&b.ctl[XA_CTL_NQ], 1u);
 				b.queue[i] = Q + 1;
 			}
 		}
-		__syncthreads();
 	}
 	/* arrival ticket, as in xa_decode_fix */
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1328,22 +1339,44 @@ xa_decode_fix_batch(xa_batch_args b)
 	if (threadIdx.x == 0)
 		drain_batch(b);
 	__syncthreads();
-	for (uint32_t sid = threadIdx.x; sid < b.nstreams; sid += 256u) {
-		const xa_batch_stream &d = b.streams[sid];
-		uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
-		uint32_t *st = b.status + sid * XA_ST_WORDS;
-		const uint2 fin = b.e[d.cbase + d.nchunks - 1];
-		st[XA_ST_ERR] = sc[XA_SCTL_ERR];
-		st[XA_ST_STATE_L] = fin.x;
-		st[XA_ST_STATE_R] = fin.y;
-		st[XA_ST_FIXED] = sc[XA_SCTL_FIXED];
-		st[XA_ST_TAIL] = sc[XA_SCTL_TAIL];
-		st[XA_ST_CHUNKS] = d.nchunks;
-		st[XA_ST_C] = d.C;
-		st[XA_ST_W] = b.W;
-		sc[XA_SCTL_ERR] = 0xffffffffu;
-		sc[XA_SCTL_FIXED] = 0;
-		sc[XA_SCTL_TAIL] = 0;
+	/* every stream's status: up to XA_PUB streams per thread, each loaded
+	 * in full before any is written, so the dependent loads (descriptor,
+	 * then the last chunk's exit state) overlap across streams */
+	constexpr int XA_PUB = 4;
+	for (uint32_t s0 = 0; s0 < b.nstreams; s0 += 256u * XA_PUB) {
+		uint32_t err[XA_PUB], fix[XA_PUB], tail[XA_PUB], nch[XA_PUB], cc[XA_PUB];
+		uint2 fin[XA_PUB];
+#pragma unroll
+		for (int k = 0; k < XA_PUB; k++) {
+			const uint32_t sid = min(s0 + threadIdx.x + 256u * k, b.nstreams - 1);
+			const xa_batch_stream &d = b.streams[sid];
+			const uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
+			nch[k] = d.nchunks;
+			cc[k] = d.C;
+			fin[k] = b.e[d.cbase + d.nchunks - 1];
+			err[k] = sc[XA_SCTL_ERR];
+			fix[k] = sc[XA_SCTL_FIXED];
+			tail[k] = sc[XA_SCTL_TAIL];
+		}
+#pragma unroll
+		for (int k = 0; k < XA_PUB; k++) {
+			const uint32_t sid = s0 + threadIdx.x + 256u * k;
+			if (sid >= b.nstreams)
+				continue;
+			uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
+			uint32_t *st = b.status + sid * XA_ST_WORDS;
+			st[XA_ST_ERR] = err[k];
+			st[XA_ST_STATE_L] = fin[k].x;
+			st[XA_ST_STATE_R] = fin[k].y;
+			st[XA_ST_FIXED] = fix[k];
+			st[XA_ST_TAIL] = tail[k];
+			st[XA_ST_CHUNKS] = nch[k];
+			st[XA_ST_C] = cc[k];
+			st[XA_ST_W] = b.W;
+			sc[XA_SCTL_ERR] = 0xffffffffu;
+			sc[XA_SCTL_FIXED] = 0;
+			sc[XA_SCTL_TAIL] = 0;
+		}
 	}
 	if (threadIdx.x == 0) {
 		b.ctl[XA_CTL_NQ] = 0;
@@ -1356,9 +1389,8 @@ xa_decode_batch_launch(const xa_batch_args &b, hipStream_t st, hipEvent_t ev0,
     hipEvent_t ev1)
 {
 	const unsigned grid = (b.nwaves + XA_SPEC_WPB - 1) / XA_SPEC_WPB;
-	const uint64_t nch = 64ull * b.nwaves;
-	unsigned grid2 = (unsigned)((nch + 256u * XA_FIX_CPT - 1) /
-	    (256u * XA_FIX_CPT));
+	/* K2: a wave per global wave, 4 per workgroup, at most 256 workgroups */
+	unsigned grid2 = (b.nwaves + 3u) / 4u;
 	if (grid2 > 256u)
 		grid2 = 256u;
 	if (ev0 != NULL)

@@ -60,11 +60,12 @@ def main():
         if args.wl.startswith("C3x"):
             # C3's 5M eblocks as n separately allocated streams (C3x<n>)
             n = int(args.wl[3:])
-            inputs = [(i, 8, 2, 5_000_000 // n, synth.stream(5_000_000 // n, 8, 2, "A",
+            inputs = [(i, 8, 2, 5_000_000 // n, synth.stream(5_000_000 // n, 8, 2, args.mix,
                                                             seed=1000 + i))
                       for i in range(n)]
         else:
-            inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)))
+            inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)),
+                                        mix=args.mix)
         if args.layout in ("packed", "gaps"):
             # every stream in one allocation, back to back at 256-B steps
             # (gaps: plus a seeded random gap of 0-255 x 256 B before each)
