@@ -38,46 +38,72 @@ def _unpack(words):
     return tuple(out)
 
 
+NO_ERROR = 1 << 62
+
+
 def resolve(local_decode, lo, hi, init_state, warmup, group=None):
     """Run the split-decode protocol for this rank's range [lo, hi).
 
     local_decode(first, state) decodes eblocks [first, hi) of the stream
-    starting from `state` and returns (state at lo, exit state at hi); it
-    is called with first = max(lo - warmup, 0) and state (0,0,0,0) for the
-    speculative pass (the stream's init_state when first == 0), and with
-    first = lo and the true entry state for a re-decode.  Its PCM output
-    for [lo, hi) must be left in place by the last call.
+    starting from `state` and returns (state at lo, exit state at hi) or
+    (state at lo, exit state, bad), where bad is the stream-global index
+    (eblock * channels + channel) of the first channel block in [lo, hi)
+    whose gain nibble is >= 5, and the exit state is then the one the
+    reference carries out of a failing call: the state after the last
+    good eblock, with the left channel of the bad eblock applied when the
+    right block is the bad one (src/libbjxa.c:633-643).  It is called with
+    first = max(lo - warmup, 0) and state (0,0,0,0) for the speculative
+    pass (the stream's init_state when first == 0), and with first = lo and
+    the true entry state for a re-decode.  Its PCM output for [lo, hi)
+    must be left in place by the last call.
 
-    Returns the stream's exit state (every rank gets the same value).
+    Returns (exit state, bad): the stream's exit state and None, or -- the
+    reference's first-bad-block semantics -- the carried state at the first
+    bad channel block of the whole stream and its index (every rank gets
+    the same value).  Ranks after the failing one are never re-decoded;
+    their PCM lies past the error.
     """
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+
+    def call(first, state):
+        res = tuple(local_decode(first, state))
+        g, e = res[0], res[1]
+        bad = res[2] if len(res) > 2 and res[2] is not None else NO_ERROR
+        return g, e, bad
+
     first = max(lo - warmup, 0)
-    g, e = local_decode(first, init_state if first == 0 else (0, 0, 0, 0))
+    g, e, bad = call(first, init_state if first == 0 else (0, 0, 0, 0))
     if rank == 0:
         g = init_state          # the true entry state, by definition
-    mine = torch.tensor(list(_pack(g)) + list(_pack(e)), dtype=torch.int64)
+
+    def pack(g, e, bad):
+        return torch.tensor(list(_pack(g)) + list(_pack(e)) + [bad], dtype=torch.int64)
+    mine = pack(g, e, bad)
     true_init = torch.tensor(list(_pack(init_state)), dtype=torch.int64)
     while True:
-        parts = [torch.zeros(4, dtype=torch.int64) for _ in range(world)]
+        parts = [torch.zeros(5, dtype=torch.int64) for _ in range(world)]
         dist.all_gather(parts, mine, group=group)
         # walk the chain: the first rank whose entry state differs from its
-        # predecessor's exit must re-decode; later ranks wait for it
+        # predecessor's exit must re-decode; later ranks wait for it.  The
+        # walk ends at the first rank that holds a bad block.
         t = true_init
         redo = None
         for r in range(world):
             if not torch.equal(parts[r][:2], t):
                 redo = r
                 break
-            t = parts[r][2:]
+            if int(parts[r][4]) != NO_ERROR:
+                return _unpack([int(v) for v in parts[r][2:4]]), int(parts[r][4])
+            t = parts[r][2:4]
         if redo is None:
-            return _unpack([int(v) for v in parts[world - 1][2:]])
+            return _unpack([int(v) for v in parts[world - 1][2:4]]), None
         if rank == redo:
             g = _unpack([int(v) for v in t])
-            _, e = local_decode(lo, g)
-            mine = torch.tensor(list(_pack(g)) + list(_pack(e)), dtype=torch.int64)
+            _, e, bad = call(lo, g)
+            mine = pack(g, e, bad)
 
 
 def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channels,
@@ -94,7 +120,14 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
     w0 = max(lo - warmup, 0)
     ebsz = (bits * 4 + 1) * ch
 
-    def decode(first, state):
+    def frame_state(dst, eblock, first, chans):
+        """(p0, p1) of each channel in `chans` after eblock `eblock` (its
+        frames 30, 31), from the PCM decoded from eblock `first` on"""
+        off = (eblock - first) * 64 * ch + 30 * 2 * ch
+        f = device_bytes(dst + off, 4 * ch).view(np.int16).reshape(2, ch)
+        return {c: (int(f[1][c]), int(f[0][c])) for c in chans}
+
+    def run(first, state):
         n = hi - first
         fr = min(frames, hi * 32) - first * 32
         src = d_src_range + (first - w0) * ebsz
@@ -106,19 +139,34 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
         bjxa_amd.decode_device(src, dst, n, fr, bits, ch, ws.data_ptr(), ws_len,
                                st.data_ptr(), state, stream=stream)
         torch.cuda.synchronize()
-        words = st.cpu().numpy().view(np.uint32)
-        if words[0] != bjxa_amd.NO_ERROR:
-            raise bjxa_amd.BjxaError(71, "decode_split: gain >= 5 in rank range")
-        exit_state = _unpack([int(words[1]), int(words[2])])
+        return dst, st.cpu().numpy().view(np.uint32).copy()
+
+    def decode(first, state):
+        dst, words = run(first, state)
         if first == lo:
-            return state, exit_state
-        # state at lo: frames 30, 31 of eblock lo - 1 are (p1, p0)
-        off = (lo - 1 - first) * 64 * ch + 30 * 2 * ch
-        f = device_bytes(dst + off, 4 * ch).view(np.int16).reshape(2, ch)
-        at_lo = []
-        for c in range(2):
-            at_lo += [int(f[1][c]) if c < ch else 0, int(f[0][c]) if c < ch else 0]
-        return tuple(at_lo), exit_state
+            at_lo = state
+        else:
+            # state at lo: frames 30, 31 of eblock lo - 1 are (p1, p0)
+            s = frame_state(dst, lo - 1, first, range(ch))
+            at_lo = tuple(v for c in range(2) for v in (s[c] if c < ch else (0, 0)))
+        err = int(words[0])
+        if err != bjxa_amd.NO_ERROR and first + err // ch < lo:
+            # the first bad block lies in the warm-up, which is the previous
+            # rank's to report: look for one in [lo, hi) from lo
+            dst, words = run(lo, at_lo)
+            first, err = lo, int(words[0])
+        if err == bjxa_amd.NO_ERROR:
+            return at_lo, _unpack([int(words[1]), int(words[2])]), None
+        # the reference stops before the failing eblock j; a bad right
+        # block leaves the left channel advanced through eblock j
+        j, bad_c = first + err // ch, err % ch
+        carried = {c: (v[2 * c], v[2 * c + 1]) for c, v in ((c, at_lo) for c in range(ch))}
+        if j > first:
+            carried.update(frame_state(dst, j - 1, first, range(ch)))
+        if ch == 2 and bad_c == 1:
+            carried.update(frame_state(dst, j, first, [0]))
+        out = tuple(v for c in range(2) for v in (carried[c] if c < ch else (0, 0)))
+        return at_lo, out, j * ch + bad_c
 
     return decode
 

@@ -89,14 +89,23 @@ def test_c5_shards_cover_the_job(world):
     assert max(sizes) - min(sizes) <= 1
 
 
-def _split_worker(rank, world, port, q, eb, bits, ch, mix, warmup, frames, init):
+def _neutral(xa, bits, ch):
+    """the stream with every gain nibble >= 5 cleared (what a speculative
+    warm-up through a bad block amounts to: the kernels decode it with K = 0)"""
+    x = xa.copy().reshape(-1, bits * 4 + 1)
+    bad = x[:, 0] >= 0x50
+    x[bad, 0] &= 0x0F
+    return x.reshape(-1)
+
+
+def _split_worker(rank, world, port, q, eb, bits, ch, mix, warmup, frames, init, bad):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import oracle
-        from bjxa_amd import dist as bdist, synth
-        xa = synth.stream(eb, bits, ch, mix, seed=77)
+        from bjxa_amd import dist as bdist
+        xa = _split_stream(eb, bits, ch, mix, bad)
         ebsz = (bits * 4 + 1) * ch
         lo, hi = bdist.split_ranges(eb, world)[rank]
         out = {}
@@ -106,37 +115,54 @@ def _split_worker(rank, world, port, q, eb, bits, ch, mix, warmup, frames, init)
             calls.append(first)
             st = state
             if first < lo:
-                _, st, _, _ = oracle.decode(xa[first * ebsz:lo * ebsz].copy(), lo - first,
-                                            bits, ch, state)
+                w = _neutral(xa[first * ebsz:lo * ebsz], bits, ch)
+                _, st, _, _ = oracle.decode(w, lo - first, bits, ch, state)
             fr = min(frames, hi * 32) - lo * 32
-            pcm, ex, _, _ = oracle.decode(xa[lo * ebsz:hi * ebsz].copy(), hi - lo, bits, ch,
-                                          st, fr)
+            pcm, ex, done, badc = oracle.decode(xa[lo * ebsz:hi * ebsz].copy(), hi - lo, bits,
+                                                ch, st, fr)
             out["pcm"] = pcm
+            if done < hi - lo:
+                return st, ex, (lo + done) * ch + badc
             return st, ex
 
-        fin = bdist.resolve(local_decode, lo, hi, init, warmup)
-        q.put((rank, out["pcm"].tobytes(), fin, len(calls)))
+        fin, fbad = bdist.resolve(local_decode, lo, hi, init, warmup)
+        q.put((rank, out["pcm"].tobytes(), fin, len(calls), fbad))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,eb,bits,ch,mix,warmup", [
-    (2, 3000, 8, 2, "A", 8), (3, 3001, 6, 1, "W", 2), (3, 4000, 4, 2, "W", 0),
-    (3, 10, 8, 2, "A", 8)])
-def test_single_stream_split(world, eb, bits, ch, mix, warmup):
+def _split_stream(eb, bits, ch, mix, bad):
+    """seeded stream; `bad` = (eblock, channel) gets gain nibble 5"""
+    from bjxa_amd import synth
+    xa = synth.stream(eb, bits, ch, mix, seed=77)
+    if bad is not None:
+        xa[(bad[0] * ch + bad[1]) * (bits * 4 + 1)] = 0x53
+    return xa
+
+
+@pytest.mark.parametrize("world,eb,bits,ch,mix,warmup,bad", [
+    (2, 3000, 8, 2, "A", 8, None), (3, 3001, 6, 1, "W", 2, None),
+    (3, 4000, 4, 2, "W", 0, None), (3, 10, 8, 2, "A", 8, None),
+    (3, 3000, 8, 2, "W", 8, (1500, 1)), (3, 3000, 8, 2, "A", 8, (1000, 0)),
+    (2, 3001, 6, 1, "W", 8, (1505, 0)), (2, 3001, 6, 1, "W", 8, (1495, 0)),
+    (3, 3000, 4, 2, "A", 8, (2999, 1))])
+def test_single_stream_split(world, eb, bits, ch, mix, warmup, bad):
     """bjxa_amd.dist.resolve: a stream split over ranks, each decoding its
     range speculatively (warm-up from (0,0)) and re-decoding when the
     all-gathered chain of states says its entry was wrong, equals the
-    single-pass decode; ranges shorter than the warm-up start at eblock 0."""
+    single-pass decode; ranges shorter than the warm-up start at eblock 0.
+    With a bad profile the result is the reference's first-bad-block
+    outcome: its index, the carried state (a bad right block leaves the
+    left channel advanced), and the PCM before it -- including a bad block
+    at the first eblock of a range or inside the next rank's warm-up."""
     import oracle
-    from bjxa_amd import synth
     frames = eb * 32 - 5
     init = (11, -22, 33, -44) if ch == 2 else (11, -22, 0, 0)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_split_worker, args=(r, world, port, q, eb, bits, ch, mix,
-                                                       warmup, frames, init))
+                                                       warmup, frames, init, bad))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -144,12 +170,20 @@ def test_single_stream_split(world, eb, bits, ch, mix, warmup):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    xa = synth.stream(eb, bits, ch, mix, seed=77)
-    ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, init, frames)
-    assert b"".join(r[1] for r in res) == ref.tobytes()
+    xa = _split_stream(eb, bits, ch, mix, bad)
+    ref, st_ref, done, badc = oracle.decode(xa, eb, bits, ch, init, frames)
     for r in res:
         assert tuple(r[2])[:2 * ch] == tuple(st_ref)[:2 * ch]
-    if mix == "W" and eb > 100:
+    joined = b"".join(r[1] for r in res)
+    if bad is None:
+        assert joined == ref.tobytes()
+        assert all(r[4] is None for r in res)
+    else:
+        assert done == bad[0] and badc == bad[1]
+        n = done * 32 * ch * 2
+        assert joined[:n] == ref.tobytes()[:n]
+        assert all(r[4] == bad[0] * ch + bad[1] for r in res)
+    if mix == "W" and eb > 100 and bad is None:
         assert any(r[3] > 1 for r in res)      # some rank had to re-decode
 
 
