@@ -7,9 +7,11 @@
  * <sys/types.h> (for ssize_t) first.  Every entry point returns -1 (or
  * NULL) and sets errno on failure; see bjxa.3 for the errno contract.
  *
- * Decoding and encoding run on the GPU (hand-written gfx950 kernels); the
- * framing functions are host C.  A process without a usable GPU gets
- * errno = ENODEV from bjxa_decode()/bjxa_encode().
+ * Decoding and encoding run on the GPU (hand-written gfx950 kernels) for
+ * calls of at least the offload threshold (bjxa_hip.h,
+ * bjxa_hip_offload_threshold) and on the calling thread's core below it and
+ * on hosts without a usable GPU; both give the reference's bytes, block
+ * counts, errno and carried state.  The framing functions are host C.
  */
 #ifndef BJXA_H_INCLUDED
 #define BJXA_H_INCLUDED

@@ -1,0 +1,45 @@
+"""bench.py's C5 line on the GPU (the driver's N > 1 headline, here at one
+rank): a small C5-shaped job through the batched kernels, the per-stream
+checksums compared with the oracle's, and the first-error stream."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+
+
+def _bench(args):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args,
+                       capture_output=True, text=True, env=env, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_c5_line_one_gpu(built):
+    rc, line, err = _bench(["--workload", "C5", "--streams", "24", "--eblocks", "3000",
+                            "--steps", "3", "--warmup", "1", "--no-other", "--no-cpu"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 1 and line["scaling"] == "strong"
+    assert line["config"]["workload_id"] == "C5" and line["config"]["streams"] == 24
+    assert line["bit_exact"] is True
+    cp = line["control_plane"]
+    assert cp["checksums_match_oracle"] is True and cp["first_error_stream"] is None
+    assert cp["shards"] == [[0, 24]]
+    assert line["roofline"]["launch_ms"] > 0 and line["value"] > 0
+
+
+def test_bench_c5_first_error_one_gpu(built):
+    rc, line, err = _bench(["--workload", "C5", "--streams", "12", "--eblocks", "2000",
+                            "--steps", "2", "--warmup", "1", "--no-other", "--no-cpu",
+                            "--bad-stream", "7"])
+    assert rc == 0, err[-2000:]
+    assert line["control_plane"]["first_error_stream"] == 7
+    assert line["control_plane"]["checksums_match_oracle"] is True
+    assert line["bit_exact"] is True
