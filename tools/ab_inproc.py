@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--mix", default="A")
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--offset", type=int, default=0,
+                    help="single-stream workloads: place src/dst this many bytes into "
+                         "larger allocations (a multiple of 16)")
     ap.add_argument("--eblocks", type=int, default=0,
                     help="single-stream workloads: override the stream length")
     ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps"],
@@ -54,10 +57,15 @@ def main():
                          "streams back to back in one allocation (packed)")
     ap.add_argument("builds", nargs="+")
     args = ap.parse_args()
-    batch = args.wl in BATCH or args.wl.startswith("C3x")
+    batch = args.wl in BATCH or args.wl.startswith(("C3x", "B"))
     if batch:
         import bench
-        if args.wl.startswith("C3x"):
+        if args.wl.startswith("B"):
+            # B<n>x<eb>: n separately allocated 8-bit stereo streams of eb eblocks
+            n, e = (int(v) for v in args.wl[1:].split("x"))
+            inputs = [(i, 8, 2, e, synth.stream(e, 8, 2, args.mix, seed=1000 + i))
+                      for i in range(n)]
+        elif args.wl.startswith("C3x"):
             # C3's 5M eblocks as n separately allocated streams (C3x<n>)
             n = int(args.wl[3:])
             inputs = [(i, 8, 2, 5_000_000 // n, synth.stream(5_000_000 // n, 8, 2, args.mix,
@@ -99,8 +107,17 @@ def main():
         eb, bits, ch = WL[args.wl]
         eb = args.eblocks or eb
         xa = synth.stream(eb, bits, ch, args.mix, seed=0)
-        src = torch.from_numpy(xa).cuda()
-        dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+        if args.offset:
+            # stream buffers placed `offset` bytes into larger allocations
+            o = args.offset
+            sbig = torch.empty(xa.size + o, dtype=torch.uint8, device="cuda")
+            dbig = torch.empty(eb * 64 * ch + o, dtype=torch.uint8, device="cuda")
+            src = sbig[o:o + xa.size]
+            src.copy_(torch.from_numpy(xa))
+            dst = dbig[o:o + eb * 64 * ch]
+        else:
+            src = torch.from_numpy(xa).cuda()
+            dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
         st = torch.zeros(8, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
     hip = ctypes.CDLL("libamdhip64.so.7")
