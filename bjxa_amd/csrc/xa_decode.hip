@@ -753,19 +753,22 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 				r[i] = src[min(d0 + i, ndw - 1)];
 		}
 	};
-	/* old end state of every channel of block b (frames 30, 31), clamped
-	 * to the last whole block: a stream whose last block is cut is never
-	 * read past its PCM */
-	auto old_state = [&](int64_t b, uint32_t *o) {
+	/* old end state of block b: its PCM frames 30 and 31 as stored (raw, so
+	 * nothing uses the loaded words before the block's compare, PF blocks
+	 * later), clamped to the last whole block: a stream whose last block is
+	 * cut is never read past its PCM */
+	auto old_state = [&](int64_t b) {
 		const uint8_t *p = a.dst + min(b, nfull - 1) * OB;
-		if (CH == 2) {
-			const uint2 f = *(const uint2 *)(p + 120);
-			o[0] = (f.y & 0xffffu) | (f.x << 16);
-			o[CH - 1] = (f.y >> 16) | (f.x & 0xffff0000u);
-		} else {
-			const uint32_t f = *(const uint32_t *)(p + 60);
-			o[0] = (f >> 16) | (f << 16);
-		}
+		if (CH == 2)
+			return *(const uint2 *)(p + 120);
+		return make_uint2(*(const uint32_t *)(p + 60), 0u);
+	};
+	/* does the state in p0/p1 equal the raw frames f? */
+	auto same_state = [&](uint2 f) {
+		if (CH == 2)
+			return f.x == (((uint32_t)p1[0] & 0xffffu) | ((uint32_t)p1[CH - 1] << 16)) &&
+			    f.y == (((uint32_t)p0[0] & 0xffffu) | ((uint32_t)p0[CH - 1] << 16));
+		return f.x == (((uint32_t)p1[0] & 0xffffu) | ((uint32_t)p0[0] << 16));
 	};
 	auto none = [](int) {};
 	/* decode eblock b from its window r, PCM to `out` (16-B pieces) */
@@ -781,38 +784,31 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 
 	constexpr int PF = XA_FIX_PF;
 	const int64_t bf = min(b1, nfull);
-	uint32_t ring[PF][WN + 1], rold[PF][CH];
+	uint32_t ring[PF][WN + 1];
+	uint2 rold[PF];
 #pragma unroll
 	for (int j = 0; j < PF; j++) {
 		fetch(ring[j], b0 + j);
-		old_state(b0 + j, rold[j]);
+		rold[j] = old_state(b0 + j);
 	}
-	bool met = false;
+	/* every slot's loaded words are first used PF blocks after their load,
+	 * in straight-line code under the lane's `act` mask, so the waits are
+	 * counted ones (no join block consumes a pending load) */
+	bool met = false, act = b0 < bf;
 	int64_t b = b0;
-	while (b < bf) {
-		bool stop = false;
+	while (act) {
 #pragma unroll
 		for (int j = 0; j < PF; j++) {
-			if (stop)
-				break;
-			decode(ring[j], b, a.dst + (uint64_t)b * OB);
-			bool m = b + 1 < eblocks;
-#pragma unroll
-			for (int c = 0; c < CH; c++)
-				m = m && xa_pack_state(p0[c], p1[c]) == rold[j][c];
-			/* refill before the exits: no load under a branch */
-			fetch(ring[j], b + PF);
-			old_state(b + PF, rold[j]);
-			b++;
-			if (m) {
-				met = true;
-				stop = true;
-			} else if (b >= bf) {
-				stop = true;
+			if (act) {
+				decode(ring[j], b, a.dst + (uint64_t)b * OB);
+				const bool m = b + 1 < eblocks && same_state(rold[j]);
+				fetch(ring[j], b + PF);
+				rold[j] = old_state(b + PF);
+				b++;
+				met = m;
+				act = !m && b < bf;
 			}
 		}
-		if (stop)
-			break;
 	}
 	if (!met && b < b1) {
 		/* b == eblocks - 1, PCM cut short: no later block to meet */
@@ -894,6 +890,10 @@ drain_tail(const xa_dec_args &a)
 		if (s.x == gq.x && s.y == gq.y)
 			continue;
 		tail++;
+#ifdef XA_DBG_NOTAIL
+		/* timing diagnostic only: leaves cascaded chunks unrepaired */
+		continue;
+#endif
 		uint2 ex;
 		const bool met = fix_chunk<BITS, CH, BUF>(a, q, s, ex);
 		a.g[q] = s;

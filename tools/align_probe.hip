@@ -1,0 +1,180 @@
+/*
+ * align_probe.hip -- does K1's input pattern pay for runs that straddle
+ * 128-B lines?  The k_skel2 skeleton of pattern_probe.hip (a lane's input
+ * for a super-step is one contiguous run, landed half a wave at a time by
+ * LDS-DMA, kept in VGPRs; output staged in LDS and stored 8 whole lines per
+ * instruction) with the run length RUNB, the lane stride and a base offset
+ * as parameters:
+ *   264 B runs at a 2640-B lane stride   (K1 on C3: runs start anywhere)
+ *   256 B runs at a 2560-B stride, base 0 (every run two whole lines)
+ *   256 B runs, base 64 / base 8          (same bytes, straddling lines)
+ *   384 B runs at a 3840-B stride, base 0 (three whole lines)
+ * Prints JSON lines (ms, TB/s of in+out bytes).
+ *
+ * build: hipcc --offload-arch=gfx950 -O3 -o align_probe tools/align_probe.hip
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+	fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+__device__ __forceinline__ void
+dma16(const void *g, uint8_t *l)
+{
+	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 16, 0, 0);
+}
+
+/* RUNB bytes per lane per super-step (two output steps of 256 B each) */
+template <int RUNB>
+__global__ __launch_bounds__(256, 2) void
+k_run(const uint8_t *src, uint8_t *dst, uint32_t nS)
+{
+	constexpr int RUN = (RUNB + 15) / 16 * 16, NPR = RUN / 16, HALF = 32 * RUN,
+	    NI = (32 * NPR + 63) / 64, LASTL = 32 * NPR - 64 * (NI - 1),
+	    RD = RUNB / 4, LINE = 144, OS = 64 * LINE;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * (HALF + OS)];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *land = lds + wv * (HALF + OS), *ost = land + HALF;
+	const uint64_t w = blockIdx.x * 4u + wv;
+	const uint32_t CBI = nS * RUNB, CBO = nS * 512u;
+	uint32_t voff[NI];
+#pragma unroll
+	for (int i = 0; i < NI; i++) {
+		const int k = i * 64 + lane;
+		voff[i] = (uint32_t)(k / NPR) * CBI + (uint32_t)(k % NPR) * 16u;
+	}
+	const uint8_t *wbi = src + w * 64ull * CBI;
+	uint8_t *wbo = dst + w * 64ull * CBO;
+	auto issue = [&](uint32_t S, int h) {
+		const uint8_t *b = wbi + (uint64_t)h * 32u * CBI + (uint64_t)S * RUNB;
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			if (i == NI - 1 && lane >= LASTL)
+				break;
+			dma16(b + voff[i], land + i * 1024);
+		}
+	};
+	uint32_t cur[RD], nxt[RD];
+	auto take = [&](int h) {
+		if ((lane >> 5) == h) {
+			const uint32_t *m = (const uint32_t *)(land + (lane & 31) * RUN);
+#pragma unroll
+			for (int i = 0; i < RD; i++)
+				nxt[i] = m[i];
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	};
+	issue(0, 0);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(0);
+	issue(0, 1);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(1);
+#pragma unroll
+	for (int i = 0; i < RD; i++)
+		cur[i] = nxt[i];
+	if (nS > 1)
+		issue(1, 0);
+	auto emit = [&](uint32_t s, const uint32_t *win) {
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			u32x4 v[8];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const int i = h * 32 + q * 4 + j;
+					v[q][j] = win[i % (RD / 2)] ^ (uint32_t)i;
+				}
+			uint8_t *line = ost + lane * LINE;
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				*(u32x4 *)(line + q * 16) = v[q];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+			for (int i = 0; i < 8; i++) {
+				const int ln = i * 8 + lane / 8, pc = lane % 8;
+				const u32x4 x = *(const u32x4 *)(ost + ln * LINE + pc * 16);
+				uint8_t *o = wbo + (uint64_t)ln * CBO + s * 256u + h * 128u + pc * 16u;
+				__builtin_nontemporal_store(x, (u32x4 *)o);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+	};
+	for (uint32_t S = 0; S < nS; S++) {
+		const bool more = S + 1 < nS;
+		if (more) {
+			if (S == 0)
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			take(0);
+			issue(S + 1, 1);
+		}
+		emit(2 * S, cur);
+		if (more) {
+			asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			take(1);
+			if (S + 2 < nS)
+				issue(S + 2, 0);
+		}
+		emit(2 * S + 1, cur + RD / 2);
+#pragma unroll
+		for (int i = 0; i < RD; i++)
+			cur[i] = nxt[i];
+	}
+}
+
+template <int RUNB>
+static void
+run(const uint8_t *src, uint8_t *dst, uint32_t base, uint32_t nS, const char *tag)
+{
+	const uint32_t lanes = 125440;
+	const unsigned grid = lanes / 256;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL(k_run<RUNB>, dim3(grid), dim3(256), 0, 0, src + base, dst, nS);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL(k_run<RUNB>, dim3(grid), dim3(256), 0, 0, src + base, dst, nS);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)lanes * nS * (RUNB + 512);
+	printf("{\"case\": \"%s\", \"run\": %d, \"base\": %u, \"supersteps\": %u, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    tag, RUNB, base, nS, ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
+int
+main()
+{
+	uint8_t *src, *dst;
+	CHECK(hipMalloc(&src, 500000000));
+	CHECK(hipMalloc(&dst, 700000000));
+	CHECK(hipMemset(src, 1, 500000000));
+	for (int rep = 0; rep < 2; rep++) {
+		run<264>(src, dst, 0, 10, "K1 C3 runs");
+		run<256>(src, dst, 0, 10, "two whole lines");
+		run<256>(src, dst, 64, 10, "256 at +64");
+		run<256>(src, dst, 8, 10, "256 at +8");
+		run<264>(src, dst, 120, 10, "264 at +120");
+		run<256>(src, dst, 0, 10, "two whole lines");
+	}
+	CHECK(hipDeviceSynchronize());
+	return 0;
+}
