@@ -47,6 +47,9 @@ Reported:
 CPU rehearsal: BJXA_BENCH_BACKEND=gloo runs the N > 1 path on CPU (gloo,
 small job via --streams/--eblocks), decoding each rank's share with the
 library's host API on its CPU core; tests/test_dist.py drives it.
+BJXA_BENCH_BACKEND=gloo-gpu runs it on a one-GPU box: every rank decodes its
+share with the batched kernels on GPU 0 and the control plane runs over
+gloo (tests/test_gpu_bench.py drives it at 2 and 3 ranks).
 """
 import argparse
 import ctypes
@@ -556,6 +559,18 @@ def main():
         if world > 1:
             dist.init_process_group("gloo")
         return main_c5_cpu(args, dev, world, rank)
+    if backend == "gloo-gpu":
+        # rehearsal of the N > 1 GPU path on a one-GPU box: every rank
+        # decodes its share on GPU 0, the control plane runs over gloo
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        if world > 1:
+            dist.init_process_group("gloo")
+        try:
+            return main_c5(args, dev, world, rank, cdev=torch.device("cpu"))
+        finally:
+            if world > 1:
+                dist.destroy_process_group()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -647,6 +662,9 @@ def main_stream(args, workload, dev, world, rank):
     }
     if other:
         line["other_configs"] = other
+    if cdev.type != dev.type:
+        line["device"] = ("rehearsal: all %d ranks share GPU 0 (control plane over gloo); "
+                          "the times are not a scaling measurement" % world)
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0 if ok in (None, True) else 1
@@ -701,23 +719,26 @@ def checksum_report(job):
     return h, match
 
 
-def main_c5(args, dev, world, rank):
+def main_c5(args, dev, world, rank, cdev=None):
     """C5: the fixed job of 1024 8-bit stereo streams (65,536 eblocks each)
-    split over the ranks -- strong scaling, no data-path collective."""
+    split over the ranks -- strong scaling, no data-path collective.  `cdev`:
+    the device of the control-plane tensors (the GPU under RCCL, the CPU
+    under gloo)."""
+    cdev = cdev or dev
     nstreams = args.streams or 1024
     r = run_batch("C5", args.steps, args.warmup, dev, not args.no_verify, nstreams, rank,
                   world, args.eblocks, bad_stream=args.bad_stream)
     elapsed, ok = r["elapsed"], r["bit_exact"]
     if world > 1:
-        elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
-    job = c5_control_plane(r, dev, world, nstreams)
+        elapsed, ok = reduce_over_ranks(elapsed, ok, cdev)
+    job = c5_control_plane(r, cdev, world, nstreams)
     digest, match = checksum_report(job)
     if match is False:
         ok = False
     # per-rank kernel times for the report
     import torch
     import torch.distributed as dist
-    lm = torch.tensor([r["spec_ms"], r["frac"]], dtype=torch.float64, device=dev)
+    lm = torch.tensor([r["spec_ms"], r["frac"]], dtype=torch.float64, device=cdev)
     parts = [torch.zeros_like(lm) for _ in range(world)]
     if world > 1:
         dist.all_gather(parts, lm)
@@ -728,7 +749,7 @@ def main_c5(args, dev, world, rank):
     other = {}
     if not args.no_other and world > 1:
         o = run_workload("C3", args, dev, world, rank, not args.no_verify, False)
-        el, ok3 = reduce_over_ranks(o["elapsed"], o["ok"], dev)
+        el, ok3 = reduce_over_ranks(o["elapsed"], o["ok"], cdev)
         o["elapsed"] = el
         o["ok"] = ok3
         other["C3_weak"] = other_stream_line(o, args.steps, world)
@@ -765,6 +786,9 @@ def main_c5(args, dev, world, rank):
     }
     if other:
         line["other_configs"] = other
+    if cdev.type != dev.type:
+        line["device"] = ("rehearsal: all %d ranks share GPU 0 (control plane over gloo); "
+                          "the times are not a scaling measurement" % world)
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0 if ok in (None, True) else 1

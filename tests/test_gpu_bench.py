@@ -43,3 +43,46 @@ def test_bench_c5_first_error_one_gpu(built):
     assert line["control_plane"]["first_error_stream"] == 7
     assert line["control_plane"]["checksums_match_oracle"] is True
     assert line["bit_exact"] is True
+
+
+def test_bench_c5_two_ranks_shared_gpu(built):
+    """The N > 1 path of bench.py on one GPU: `--gpus 2` starts its own two
+    ranks, each decodes its share of the job with the batched kernels on
+    GPU 0, and the control plane (gloo here, RCCL on a node) gathers the
+    checksums, the first failing stream and the per-rank C3 lines."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["BJXA_BENCH_BACKEND"] = "gloo-gpu"
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--workload", "C5", "--streams", "20", "--eblocks", "3000",
+                        "--steps", "3", "--warmup", "1", "--no-cpu", "--bad-stream", "13"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, r.stderr[-3000:]
+    line = json.loads(lines[-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert "rehearsal" in line["device"]
+    cp = line["control_plane"]
+    assert cp["shards"] == [[0, 10], [10, 20]]
+    assert cp["first_error_stream"] == 13
+    assert cp["checksums_match_oracle"] is True and line["bit_exact"] is True
+    c3 = line["other_configs"]["C3_weak"]
+    assert c3["bit_exact"] is True and c3["value"] > 0
+
+
+def test_bench_c5_three_ranks_shared_gpu(built):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["BJXA_BENCH_BACKEND"] = "gloo-gpu"
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "3",
+                        "--workload", "C5", "--streams", "17", "--eblocks", "2500",
+                        "--steps", "2", "--warmup", "1", "--no-cpu", "--no-other"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, r.stderr[-3000:]
+    line = json.loads(lines[-1])
+    assert line["n_gpus"] == 3
+    assert line["control_plane"]["shards"] == [[0, 5], [5, 11], [11, 17]]
+    assert line["control_plane"]["first_error_stream"] is None
+    assert line["control_plane"]["checksums_match_oracle"] is True
+    assert line["bit_exact"] is True
