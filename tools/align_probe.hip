@@ -29,13 +29,15 @@ dma16(const void *g, uint8_t *l)
 }
 
 /* RUNB bytes per lane per super-step (two output steps of 256 B each) */
-template <int RUNB>
+template <int RUNB, bool LINES = false>
 __global__ __launch_bounds__(256, 2) void
 k_run(const uint8_t *src, uint8_t *dst, uint32_t nS)
 {
-	constexpr int RUN = (RUNB + 15) / 16 * 16, NPR = RUN / 16, HALF = 32 * RUN,
-	    NI = (32 * NPR + 63) / 64, LASTL = 32 * NPR - 64 * (NI - 1),
-	    RD = RUNB / 4, LINE = 144, OS = 64 * LINE;
+	/* LINES: land the 3 whole 128-B lines that cover each run (384 B) and
+	 * stage the output unpadded (128-B lines), 20 KiB per wave */
+	constexpr int RUN = LINES ? 384 : (RUNB + 15) / 16 * 16, NPR = RUN / 16,
+	    HALF = 32 * RUN, NI = (32 * NPR + 63) / 64, LASTL = 32 * NPR - 64 * (NI - 1),
+	    RD = RUNB / 4, LINE = LINES ? 128 : 144, OS = 64 * LINE;
 	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * (HALF + OS)];
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int lane = threadIdx.x & 63;
@@ -56,13 +58,22 @@ k_run(const uint8_t *src, uint8_t *dst, uint32_t nS)
 		for (int i = 0; i < NI; i++) {
 			if (i == NI - 1 && lane >= LASTL)
 				break;
-			dma16(b + voff[i], land + i * 1024);
+			const uint8_t *a = b + voff[i];
+			if (LINES) {
+				/* piece k of run r: the line-aligned base of run r */
+				const int k = i * 64 + lane, r = k / NPR, pc = k % NPR;
+				const uint8_t *rb = b + (uint64_t)r * CBI;
+				a = (const uint8_t *)((uintptr_t)rb & ~(uintptr_t)127) + pc * 16;
+			}
+			dma16(a, land + i * 1024);
 		}
 	};
 	uint32_t cur[RD], nxt[RD];
 	auto take = [&](int h) {
 		if ((lane >> 5) == h) {
-			const uint32_t *m = (const uint32_t *)(land + (lane & 31) * RUN);
+			const uint32_t *m = (const uint32_t *)(land + (lane & 31) * RUN +
+			    (LINES ? (((uintptr_t)wbi + (uint64_t)(lane >> 5) * 32u * CBI +
+			    (uint64_t)(lane & 31) * CBI) & 127) : 0));
 #pragma unroll
 			for (int i = 0; i < RD; i++)
 				nxt[i] = m[i];
@@ -94,14 +105,15 @@ k_run(const uint8_t *src, uint8_t *dst, uint32_t nS)
 			uint8_t *line = ost + lane * LINE;
 #pragma unroll
 			for (int q = 0; q < 8; q++)
-				*(u32x4 *)(line + q * 16) = v[q];
+				*(u32x4 *)(line + 16 * (LINES ? (q ^ (lane & 7)) : q)) = v[q];
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 			__builtin_amdgcn_wave_barrier();
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
 			for (int i = 0; i < 8; i++) {
 				const int ln = i * 8 + lane / 8, pc = lane % 8;
-				const u32x4 x = *(const u32x4 *)(ost + ln * LINE + pc * 16);
+				const u32x4 x = *(const u32x4 *)(ost + ln * LINE +
+				    16 * (LINES ? (pc ^ (ln & 7)) : pc));
 				uint8_t *o = wbo + (uint64_t)ln * CBO + s * 256u + h * 128u + pc * 16u;
 				__builtin_nontemporal_store(x, (u32x4 *)o);
 			}
@@ -134,7 +146,154 @@ k_run(const uint8_t *src, uint8_t *dst, uint32_t nS)
 	}
 }
 
-template <int RUNB>
+/*
+ * The byte-stream structure K1 would need for line-exact input: each lane's
+ * landing slot is [carry line | 2 new lines] (384 B); a super-step DMAs only
+ * the 2 new whole lines of every run (pieces that would land in a carry
+ * area are masked off: 12 instructions per half instead of 8), the lane
+ * reads its 264-B run from the slot at its own byte offset, then copies the
+ * slot's last line into the carry area for the next super-step.  Output
+ * staged unpadded with an XOR swizzle (8 KiB per wave).  Source: 256 new
+ * bytes per lane per super-step (two aligned lines), lane stride nS*256.
+ */
+__global__ __launch_bounds__(256, 2) void
+k_carry(const uint8_t *src, uint8_t *dst, uint32_t nS)
+{
+	constexpr int SLOT = 384, HALF = 32 * SLOT, NI = HALF / 1024, RD = 66,
+	    LINE = 128, OS = 64 * LINE;
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4 * (HALF + OS)];
+	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	uint8_t *land = lds + wv * (HALF + OS), *ost = land + HALF;
+	const uint64_t w = blockIdx.x * 4u + wv;
+	const uint32_t CBI = nS * 256u, CBO = nS * 512u;
+	uint32_t voff[NI];
+	bool von[NI];
+#pragma unroll
+	for (int i = 0; i < NI; i++) {
+		const int k = i * 64 + lane, r = k / 24, pc = k % 24;
+		von[i] = pc >= 8;
+		voff[i] = (uint32_t)r * CBI + (uint32_t)(pc >= 8 ? pc - 8 : 0) * 16u;
+	}
+	const uint8_t *wbi = src + w * 64ull * CBI;
+	uint8_t *wbo = dst + w * 64ull * CBO;
+	const int o = (lane * 8) & 120;		/* a run's byte offset in its slot */
+	auto issue = [&](uint32_t S, int h) {
+		const uint8_t *b = wbi + (uint64_t)h * 32u * CBI + (uint64_t)S * 256u;
+#pragma unroll
+		for (int i = 0; i < NI; i++)
+			if (von[i])
+				dma16(b + voff[i], land + i * 1024);
+	};
+	uint32_t cur[RD], nxt[RD];
+	auto take = [&](int h) {
+		if ((lane >> 5) == h) {
+			uint8_t *sl = land + (lane & 31) * SLOT;
+			const uint32_t *m = (const uint32_t *)(sl + o);
+#pragma unroll
+			for (int i = 0; i < RD; i++)
+				nxt[i] = m[i];
+			u32x4 c[8];
+#pragma unroll
+			for (int i = 0; i < 8; i++)
+				c[i] = *(const u32x4 *)(sl + 256 + 16 * i);
+#pragma unroll
+			for (int i = 0; i < 8; i++)
+				*(u32x4 *)(sl + 16 * i) = c[i];
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	};
+	issue(0, 0);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(0);
+	issue(0, 1);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	take(1);
+#pragma unroll
+	for (int i = 0; i < RD; i++)
+		cur[i] = nxt[i];
+	if (nS > 1)
+		issue(1, 0);
+	auto emit = [&](uint32_t s, const uint32_t *win) {
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			u32x4 v[8];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+#pragma unroll
+				for (int j = 0; j < 4; j++) {
+					const int i = h * 32 + q * 4 + j;
+					v[q][j] = win[i % 33] ^ (uint32_t)i;
+				}
+			uint8_t *line = ost + lane * LINE;
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				*(u32x4 *)(line + 16 * (q ^ (lane & 7))) = v[q];
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+			for (int i = 0; i < 8; i++) {
+				const int ln = i * 8 + lane / 8, pc = lane % 8;
+				const u32x4 x = *(const u32x4 *)(ost + ln * LINE + 16 * (pc ^ (ln & 7)));
+				uint8_t *op = wbo + (uint64_t)ln * CBO + s * 256u + h * 128u + pc * 16u;
+				__builtin_nontemporal_store(x, (u32x4 *)op);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+	};
+	for (uint32_t S = 0; S < nS; S++) {
+		const bool more = S + 1 < nS;
+		if (more) {
+			if (S == 0)
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			take(0);
+			issue(S + 1, 1);
+		}
+		emit(2 * S, cur);
+		if (more) {
+			asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			take(1);
+			if (S + 2 < nS)
+				issue(S + 2, 0);
+		}
+		emit(2 * S + 1, cur + 33);
+#pragma unroll
+		for (int i = 0; i < RD; i++)
+			cur[i] = nxt[i];
+	}
+}
+
+static void
+run_carry(const uint8_t *src, uint8_t *dst, uint32_t nS)
+{
+	const uint32_t lanes = 125440;
+	const unsigned grid = lanes / 256;
+	hipEvent_t a, b;
+	hipEventCreate(&a);
+	hipEventCreate(&b);
+	for (int i = 0; i < 2; i++)
+		hipLaunchKernelGGL(k_carry, dim3(grid), dim3(256), 0, 0, src, dst, nS);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 20; i++)
+		hipLaunchKernelGGL(k_carry, dim3(grid), dim3(256), 0, 0, src, dst, nS);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms;
+	hipEventElapsedTime(&ms, a, b);
+	ms /= 20;
+	const double bytes = (double)lanes * nS * (256 + 512);
+	printf("{\"case\": \"carry line + 2 new lines\", \"supersteps\": %u, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    nS, ms, bytes / ms / 1e9);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+}
+
+template <int RUNB, bool LINES = false>
 static void
 run(const uint8_t *src, uint8_t *dst, uint32_t base, uint32_t nS, const char *tag)
 {
@@ -144,10 +303,10 @@ run(const uint8_t *src, uint8_t *dst, uint32_t base, uint32_t nS, const char *ta
 	hipEventCreate(&a);
 	hipEventCreate(&b);
 	for (int i = 0; i < 2; i++)
-		hipLaunchKernelGGL(k_run<RUNB>, dim3(grid), dim3(256), 0, 0, src + base, dst, nS);
+		hipLaunchKernelGGL((k_run<RUNB, LINES>), dim3(grid), dim3(256), 0, 0, src + base, dst, nS);
 	hipEventRecord(a, 0);
 	for (int i = 0; i < 20; i++)
-		hipLaunchKernelGGL(k_run<RUNB>, dim3(grid), dim3(256), 0, 0, src + base, dst, nS);
+		hipLaunchKernelGGL((k_run<RUNB, LINES>), dim3(grid), dim3(256), 0, 0, src + base, dst, nS);
 	hipEventRecord(b, 0);
 	hipEventSynchronize(b);
 	float ms;
@@ -174,6 +333,9 @@ main()
 		run<256>(src, dst, 8, 10, "256 at +8");
 		run<264>(src, dst, 120, 10, "264 at +120");
 		run<256>(src, dst, 0, 10, "two whole lines");
+		run<264, true>(src, dst, 0, 10, "264 via 3 whole lines");
+		run<264, true>(src, dst, 120, 10, "264 via 3 whole lines, +120");
+		run_carry(src, dst, 10);
 	}
 	CHECK(hipDeviceSynchronize());
 	return 0;
