@@ -662,9 +662,6 @@ def main_stream(args, workload, dev, world, rank):
     }
     if other:
         line["other_configs"] = other
-    if cdev.type != dev.type:
-        line["device"] = ("rehearsal: all %d ranks share GPU 0 (control plane over gloo); "
-                          "the times are not a scaling measurement" % world)
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0 if ok in (None, True) else 1

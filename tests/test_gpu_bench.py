@@ -86,3 +86,15 @@ def test_bench_c5_three_ranks_shared_gpu(built):
     assert line["control_plane"]["first_error_stream"] is None
     assert line["control_plane"]["checksums_match_oracle"] is True
     assert line["bit_exact"] is True
+
+
+def test_bench_default_line_c3(built):
+    """The driver's N = 1 headline path (C3, main_stream) end to end: the
+    full stream, bit-exact against the oracle, roofline and its fields."""
+    rc, line, err = _bench(["--steps", "3", "--warmup", "1", "--no-other", "--no-cpu"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 1 and line["config"]["workload_id"] == "C3"
+    assert line["bit_exact"] is True and line["value"] > 0
+    rf = line["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["achieved"] > 0
+    assert "device" not in line
