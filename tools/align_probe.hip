@@ -313,16 +313,106 @@ run(const uint8_t *src, uint8_t *dst, uint32_t base, uint32_t nS, const char *ta
 	hipEventElapsedTime(&ms, a, b);
 	ms /= 20;
 	const double bytes = (double)lanes * nS * (RUNB + 512);
-	printf("{\"case\": \"%s\", \"run\": %d, \"base\": %u, \"supersteps\": %u, \"ms\": %.4f, \"TBs\": %.3f}\n",
-	    tag, RUNB, base, nS, ms, bytes / ms / 1e9);
+	printf("{\"case\": \"%s\", \"run\": %d, \"base\": %u, \"supersteps\": %u, \"pcm_stride\": %u, \"ms\": %.4f, \"TBs\": %.3f}\n",
+	    tag, RUNB, base, nS, nS * 512u, ms, bytes / ms / 1e9);
 	hipEventDestroy(a);
 	hipEventDestroy(b);
 }
 
 int
-main()
+main(int argc, char **argv)
 {
 	uint8_t *src, *dst;
+	if (argc > 1 && argv[1][0] == 'r') {
+		/* does the rate depend on where dst lies relative to src?  six
+		 * fresh buffer pairs (dst 2 MiB oversized), each timed with dst
+		 * shifted by 0 .. 1 MiB inside its allocation */
+		const size_t ni = 125440ull * 264 * 10, no = 125440ull * 512 * 10;
+		const size_t sh[] = {0, 2048, 4096, 8192, 16384, 65536, 262144, 1048576};
+		for (int k = 0; k < 6; k++) {
+			uint8_t *sk, *dk;
+			CHECK(hipMalloc(&sk, ni));
+			CHECK(hipMalloc(&dk, no + (2u << 20)));
+			CHECK(hipMemset(sk, 1, ni));
+			if (k == 3) {
+				uint8_t *d;
+				CHECK(hipMalloc(&d, 16ull << 30));
+			}
+			printf("{\"pair\": %d, \"src\": \"%p\", \"dst\": \"%p\"}\n", k, sk, dk);
+			for (size_t o : sh) {
+				char t[64];
+				snprintf(t, sizeof t, "pair %d dst+%zu", k, o);
+				run<264>(sk, dk + o, 0, 10, t);
+			}
+		}
+		return 0;
+	}
+	if (argc > 1 && argv[1][0] == 'q') {
+		/* placement, finer: exact-size buffer pairs allocated after 0, 1,
+		 * 4, 16 and 64 GiB of other allocations (all kept), timed
+		 * interleaved */
+		const size_t ni = 125440ull * 264 * 10, no = 125440ull * 512 * 10;
+		const size_t pad[] = {0, 1ull << 30, 3ull << 30, 12ull << 30, 48ull << 30};
+		const char *tag[] = {"after 0 GiB", "after 1 GiB", "after 4 GiB", "after 16 GiB", "after 64 GiB"};
+		uint8_t *si[5], *di[5];
+		for (int k = 0; k < 5; k++) {
+			if (pad[k]) {
+				uint8_t *d;
+				CHECK(hipMalloc(&d, pad[k]));
+			}
+			CHECK(hipMalloc(&si[k], ni));
+			CHECK(hipMalloc(&di[k], no));
+			CHECK(hipMemset(si[k], 1, ni));
+			CHECK(hipMemset(di[k], 0, no));
+			printf("{\"alloc\": \"%s\", \"src\": \"%p\", \"dst\": \"%p\"}\n", tag[k], si[k], di[k]);
+		}
+		for (int rep = 0; rep < 3; rep++)
+			for (int k = 0; k < 5; k++)
+				run<264>(si[k], di[k], 0, 10, tag[k]);
+		return 0;
+	}
+	if (argc > 1 && argv[1][0] == 'p') {
+		/* placement: the C3 pattern (nS = 10) on buffers allocated in
+		 * different ways */
+		const size_t ni = 125440ull * 264 * 10, no = 125440ull * 512 * 10;
+		uint8_t *s1, *d1, *big, *s3, *d3, *dummy, *s4, *d4;
+		CHECK(hipMalloc(&s1, ni));
+		CHECK(hipMalloc(&d1, no));
+		CHECK(hipMalloc(&big, 4ull << 30));
+		CHECK(hipMalloc(&s3, 125440ull * 264 * 128));
+		CHECK(hipMalloc(&d3, 125440ull * 512 * 128));
+		CHECK(hipMalloc(&dummy, 16ull << 30));
+		CHECK(hipMalloc(&s4, ni));
+		CHECK(hipMalloc(&d4, no));
+		CHECK(hipMemset(s1, 1, ni));
+		CHECK(hipMemset(big, 1, 4ull << 30));
+		CHECK(hipMemset(s3, 1, ni));
+		CHECK(hipMemset(s4, 1, ni));
+		printf("{\"ptrs\": [\"%p\", \"%p\", \"%p\", \"%p\", \"%p\", \"%p\", \"%p\"]}\n",
+		    s1, d1, big, s3, d3, s4, d4);
+		for (int rep = 0; rep < 3; rep++) {
+			run<264>(s1, d1, 0, 10, "exact-size buffers");
+			run<264>(big, big + (1ull << 30), 0, 10, "one 4 GiB buffer");
+			run<264>(s3, d3, 0, 10, "4 / 8 GB buffers");
+			run<264>(s4, d4, 0, 10, "exact-size after a 16 GiB buffer");
+			run<264>(big + (2ull << 20), big + (1ull << 30) + (6ull << 20), 0, 10, "4 GiB buffer, +2/+6 MiB");
+		}
+		return 0;
+	}
+	if (argc > 1) {
+		/* lane-stride sweep: K1's C3 pattern (264-B runs, 4 eblocks per
+		 * super-step) with nS super-steps per lane, i.e. chunks of 4 nS
+		 * eblocks at an input stride of 264 nS and a PCM stride of 512 nS
+		 * bytes, on a chip-filling grid */
+		const uint32_t ns[] = {8, 10, 12, 14, 15, 16, 17, 18, 20, 24, 30, 31, 32, 33, 48, 64, 65, 128};
+		CHECK(hipMalloc(&src, 125440ull * 264 * 128 + 4096));
+		CHECK(hipMalloc(&dst, 125440ull * 512 * 128 + 4096));
+		CHECK(hipMemset(src, 1, 125440ull * 264 * 128));
+		for (int rep = 0; rep < 2; rep++)
+			for (uint32_t n : ns)
+				run<264>(src, dst, 0, n, "stride sweep");
+		return 0;
+	}
 	CHECK(hipMalloc(&src, 500000000));
 	CHECK(hipMalloc(&dst, 700000000));
 	CHECK(hipMemset(src, 1, 500000000));
