@@ -52,6 +52,7 @@ share with the batched kernels on GPU 0 and the control plane runs over
 gloo (tests/test_gpu_bench.py drives it at 2 and 3 ranks).
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -206,6 +207,36 @@ def pcm_checksum_torch(buf_u8, n):
 
 # ---- one long stream per rank (C2/C3) ----------------------------------------
 
+def timed_serial(step, steps, dev):
+    """The same steps one at a time on slot 0 (no overlap between steps),
+    reported beside a pipelined timing; this rank only, no barrier."""
+    import torch
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(0)
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0
+
+
+def pipeline_slots(depth, dev, make):
+    """`depth` independent sets of output/workspace buffers, each with a HIP
+    stream of its own (slot 0 on torch's current stream).  Consecutive steps
+    go to consecutive slots, so step i+1's spec kernel can take the CUs that
+    step i's tail leaves idle and step i's verify/repair kernel runs beside
+    it; step i+depth reuses slot i's buffers after step i on the same
+    stream.  Every step is still a whole decode of its batch."""
+    import torch
+    slots = []
+    for k in range(max(1, depth)):
+        st = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
+        sl = make()
+        sl["stream"] = st
+        sl["sh"] = st.cuda_stream
+        slots.append(sl)
+    return slots
+
+
 def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     """Decode one seeded stream `args.steps` times (after `args.warmup`
     untimed steps), then time EV_SAMPLES more launches with events;
@@ -219,45 +250,54 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     samples = eb * 32 * ch
     xa_np = synth.stream(eb, bits, ch, args.mix, seed=rank)
     src = torch.from_numpy(xa_np).to(dev)
-    dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
     ws_len = bjxa_amd.decode_workspace_size(eb, ch, args.chunk, args.warm_blocks)
-    ws = torch.zeros(ws_len, dtype=torch.uint8, device=dev)
-    status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
-    sh = torch.cuda.current_stream(dev).cuda_stream
-    bjxa_amd.workspace_init(ws.data_ptr(), ws_len, sh)
+    slots = pipeline_slots(args.pipeline, dev, lambda: {
+        "dst": torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev),
+        "ws": torch.zeros(ws_len, dtype=torch.uint8, device=dev),
+        "status": torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)})
+    for sl in slots:
+        bjxa_amd.workspace_init(sl["ws"].data_ptr(), ws_len, sl["sh"])
+    torch.cuda.synchronize(dev)
 
-    def step(ev=(None, None)):
-        bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, bits, ch,
-                               ws.data_ptr(), ws_len, status.data_ptr(), (0, 0, 0, 0),
-                               args.chunk, args.warm_blocks, sh, ev)
+    def step(i, ev=(None, None)):
+        sl = slots[i % len(slots)]
+        bjxa_amd.decode_device(src.data_ptr(), sl["dst"].data_ptr(), eb, eb * 32, bits, ch,
+                               sl["ws"].data_ptr(), ws_len, sl["status"].data_ptr(),
+                               (0, 0, 0, 0), args.chunk, args.warm_blocks, sl["sh"], ev)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
 
+    serial = timed_serial(step, args.steps, dev) if len(slots) > 1 else elapsed
+
+    # kernel timing: slot 0 alone, one launch at a time (no overlap)
     evs = EventPairs(max(EV_SAMPLES, args.steps))
     for ev in evs.ev:
-        step(ev)
+        step(0, ev)
     spec_ms = evs.ms()
     evs.close()
-    st = status.cpu().numpy().view(np.uint32).copy()
+    torch.cuda.synchronize(dev)
+    st = slots[0]["status"].cpu().numpy().view(np.uint32).copy()
+    same = all(torch.equal(sl["dst"], slots[0]["dst"]) and
+               torch.equal(sl["status"], slots[0]["status"]) for sl in slots[1:])
 
     ok, cpu = None, None
     if verify or cpu_leg:
         import oracle
-        out = dst.cpu().numpy().view(np.int16)
+        out = slots[0]["dst"].cpu().numpy().view(np.int16)
         ref, _, _, _ = oracle.decode(xa_np, eb, bits, ch)   # also the discarded pass
-        ok = bool(np.array_equal(out, ref))
+        ok = bool(np.array_equal(out, ref)) and same
         del out
         if cpu_leg:
             times = []
@@ -275,7 +315,8 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
 
     xa_bytes = eb * ch * (bits * 4 + 1)
     return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
-            "elapsed": elapsed, "spec_ms": float(np.median(spec_ms)),
+            "elapsed": elapsed, "serial": serial, "pipeline": len(slots),
+            "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
             "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
 
@@ -349,7 +390,7 @@ def cpu_batch_baseline(name, inputs):
 
 
 def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, eblocks=0,
-              cpu_leg=False, bad_stream=-1):
+              cpu_leg=False, bad_stream=-1, pipeline=1):
     """Decode (this rank's share of) a batch config with bjxa_hip_batch_* --
     all streams per launch -- `steps` times after `warmup` untimed steps,
     then time EV_SAMPLES more launches with events.  Returns this rank's
@@ -366,44 +407,58 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
     # power-of-two spacing decode up to 30 % slower ("Stream
     # placement")
     torch.cuda.empty_cache()
-    srcs, dsts, streams = [], [], []
-    samples = alg = 0
-    for i, bits, ch, eb, xa in inputs:
-        s = torch.from_numpy(xa).to(dev)
-        d = torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
-        srcs.append(s)
-        dsts.append(d)
-        streams.append({"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
-                        "bits": bits, "channels": ch})
-        samples += eb * 32 * ch
-        alg += xa.nbytes + eb * 64 * ch
+    srcs = [torch.from_numpy(xa).to(dev) for _, _, _, _, xa in inputs]
+    samples = sum(eb * 32 * ch for _, _, ch, eb, _ in inputs)
+    alg = sum(xa.nbytes + eb * 64 * ch for _, _, ch, eb, xa in inputs)
     n = len(inputs)
-    status = torch.zeros(max(n, 1) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)
-    sh = torch.cuda.current_stream(dev).cuda_stream
-    elapsed, spec = 0.0, [0.0]
+
+    def make_slot():
+        dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
+                for _, _, ch, eb, _ in inputs]
+        return {"dsts": dsts,
+                "status": torch.zeros(max(n, 1) * bjxa_amd.STATUS_WORDS, dtype=torch.int32,
+                                      device=dev)}
+    slots = pipeline_slots(pipeline, dev, make_slot)
+    elapsed, spec, serial = 0.0, [0.0], 0.0
     if n:
-        with bjxa_amd.Batch(streams, stream=sh) as batch:
-            for _ in range(warmup):
-                batch.decode(status.data_ptr(), sh)
+        with contextlib.ExitStack() as stack:
+            for sl in slots:
+                desc = [{"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
+                         "bits": bits, "channels": ch}
+                        for s, d, (_, bits, ch, eb, _) in zip(srcs, sl["dsts"], inputs)]
+                sl["batch"] = stack.enter_context(bjxa_amd.Batch(desc, stream=sl["sh"]))
+            torch.cuda.synchronize(dev)
+
+            def step(i, ev=(None, None)):
+                sl = slots[i % len(slots)]
+                sl["batch"].decode(sl["status"].data_ptr(), sl["sh"], ev)
+            for i in range(warmup):
+                step(i)
             torch.cuda.synchronize(dev)
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
-            for _ in range(steps):
-                batch.decode(status.data_ptr(), sh)
+            for i in range(steps):
+                step(i)
             torch.cuda.synchronize(dev)
             elapsed = time.perf_counter() - t0
             if world > 1:
                 dist.barrier()
+            serial = timed_serial(step, steps, dev) if len(slots) > 1 else elapsed
+            # kernel timing: slot 0 alone, one launch at a time
             evs = EventPairs(max(EV_SAMPLES, steps))
             for ev in evs.ev:
-                batch.decode(status.data_ptr(), sh, ev)
+                step(0, ev)
             spec = evs.ms()
             evs.close()
+            torch.cuda.synchronize(dev)
     elif world > 1:
         dist.barrier()
         dist.barrier()
+    dsts, status = slots[0]["dsts"], slots[0]["status"]
+    same = all(torch.equal(sl["status"], status) and
+               all(torch.equal(a, b) for a, b in zip(sl["dsts"], dsts)) for sl in slots[1:])
     spec_ms = float(np.median(spec))
     st = status.cpu().numpy().view(np.uint32).reshape(max(n, 1), -1)[:n]
     # a failed stream counts only the PCM before its failing eblock
@@ -416,7 +471,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
     if verify:
         threads, _ = cpu_threads()
         refs, _ = oracle_batch(inputs, max(1, threads // world))
-        ok, ref_sums = True, []
+        ok, ref_sums = same, []
         for (i, bits, ch, eb, xa), d, w in zip(inputs, dsts, st):
             pcm, _, done, _ = refs[i]
             ref_sums.append(pcm_checksum_np(pcm[:done * 32 * ch]))
@@ -432,6 +487,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             "value": round(samples * steps / elapsed / 1e6, 1) if elapsed else 0.0,
             "unit": "MSamples/s",
             "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "pipeline": len(slots), "ms_per_step_serial": round(serial / steps * 1e3, 4),
             "spec_ms": round(spec_ms, 4), "spec_samples": len(spec),
             "frac": round(alg / (spec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if spec_ms else 0.0,
             "alg_bytes": alg, "repaired": int(st[:, 3].sum()) if n else 0,
@@ -531,6 +587,9 @@ def parse_args(argv=None):
     ap.add_argument("--eblocks", type=int, default=0, help="C5 eblocks per stream (65,536)")
     ap.add_argument("--bad-stream", type=int, default=-1,
                     help="C5: give this stream a gain-5 profile (first-error collective)")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="steps in flight: consecutive steps on this many HIP streams, "
+                         "each with its own output and workspace buffers")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true",
@@ -589,6 +648,7 @@ def other_stream_line(o, steps, world=1):
     return {"workload": o["desc"] + (" per rank" if world > 1 else ""),
             "value": round(job_value(o["samples"], world, steps, o["elapsed"]), 1),
             "unit": "MSamples/s", "ms_per_step": round(o["elapsed"] / steps * 1e3, 4),
+            "pipeline": o["pipeline"], "ms_per_step_serial": round(o["serial"] / steps * 1e3, 4),
             "spec_ms": round(o["spec_ms"], 4), "spec_samples": o["spec_samples"],
             "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "chunk": int(o["status"][6]), "bit_exact": o["ok"], "cpu_baseline": o["cpu"]}
@@ -612,7 +672,7 @@ def main_stream(args, workload, dev, world, rank):
             ok = ok if o["ok"] in (None, True) else False
         for name in sorted(BATCHES):
             o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify,
-                          cpu_leg=cpu_leg)
+                          cpu_leg=cpu_leg, pipeline=args.pipeline)
             for k in ("checksums", "ref_checksums", "shard"):
                 o.pop(k)
             if o["first_error"] == FIRST_ERR_NONE:
@@ -635,6 +695,7 @@ def main_stream(args, workload, dev, world, rank):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step_serial": round(r["serial"] / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -645,7 +706,8 @@ def main_stream(args, workload, dev, world, rank):
                    "eblocks_per_rank": r["eb"], "samples_per_rank": r["samples"],
                    "profile_mix": args.mix, "parallelism": "independent streams, 1 per GPU",
                    "chunk": int(st[6]), "warmup_eblocks": int(st[7]),
-                   "tuning": "auto" if not args.chunk and args.warm_blocks < 0 else "manual"},
+                   "tuning": "auto" if not args.chunk and args.warm_blocks < 0 else "manual",
+                   "pipeline": r["pipeline"]},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -724,7 +786,7 @@ def main_c5(args, dev, world, rank, cdev=None):
     cdev = cdev or dev
     nstreams = args.streams or 1024
     r = run_batch("C5", args.steps, args.warmup, dev, not args.no_verify, nstreams, rank,
-                  world, args.eblocks, bad_stream=args.bad_stream)
+                  world, args.eblocks, bad_stream=args.bad_stream, pipeline=args.pipeline)
     elapsed, ok = r["elapsed"], r["bit_exact"]
     if world > 1:
         elapsed, ok = reduce_over_ranks(elapsed, ok, cdev)
@@ -757,7 +819,8 @@ def main_c5(args, dev, world, rank, cdev=None):
         "metric": METRIC,
         "value": round(job["samples"] * args.steps / elapsed / 1e6, 1), "unit": "MSamples/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step_serial": r["ms_per_step_serial"], "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int32+f32",
         "data": "synthetic (seeded XA streams, profile mix A, uniform codes)",
         "config": {"workload": BATCHES["C5"] if not (args.streams or args.eblocks) else
@@ -766,7 +829,7 @@ def main_c5(args, dev, world, rank, cdev=None):
                    "workload_id": "C5", "streams": job["streams"],
                    "streams_per_rank": [hi - lo for lo, hi in job["shards"]],
                    "parallelism": "stream shards, one batched launch per GPU, RCCL control "
-                                  "plane only"},
+                                  "plane only", "pipeline": r["pipeline"]},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec_batch (rank 0)",
                      "achieved": round(r["alg_bytes"] / (spec_ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["frac"],

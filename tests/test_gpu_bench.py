@@ -98,3 +98,19 @@ def test_bench_default_line_c3(built):
     rf = line["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["achieved"] > 0
     assert "device" not in line
+    assert line["config"]["pipeline"] == 2 and line["ms_per_step_serial"] > 0
+
+
+def test_bench_pipeline_slots_agree(built):
+    """Three steps in flight on three HIP streams: every slot's PCM and
+    status must equal slot 0's, which is checked against the oracle."""
+    rc, line, err = _bench(["--workload", "C5", "--streams", "16", "--eblocks", "4000",
+                            "--steps", "7", "--warmup", "2", "--no-other", "--no-cpu",
+                            "--pipeline", "3"])
+    assert rc == 0, err[-2000:]
+    assert line["config"]["pipeline"] == 3 and line["bit_exact"] is True
+    assert line["control_plane"]["checksums_match_oracle"] is True
+    rc, line, err = _bench(["--workload", "C2", "--steps", "5", "--warmup", "1", "--no-other",
+                            "--no-cpu", "--pipeline", "3"])
+    assert rc == 0, err[-2000:]
+    assert line["config"]["pipeline"] == 3 and line["bit_exact"] is True

@@ -1,7 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-B="wpb4=bjxa_amd/libbjxa.so.0:0 wpb8=dbg/wpb8/libbjxa.so.0:0"
-for wl in C3 C2 C4 C5g; do
-timeout -k 10 300 python tools/ab_inproc.py --wl $wl --mix A --reps 3 --steps 20 $B > gpurun_out/e34.log 2>&1 || exit 1
-echo == $wl A; grep -v amdgpu.ids gpurun_out/e34.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_bench.py -x -q --timeout 280 --timeout-method thread > gpurun_out/p2_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/p2_tests.log; exit 1; }
+tail -2 gpurun_out/p2_tests.log
+for d in 1 2; do
+bash tools/trace.sh pipe$d --pipeline $d --steps 30 || exit 1
+python3 tools/trace_overlap.py gpurun_out/prof_pipe$d
 done
