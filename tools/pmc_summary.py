@@ -3,6 +3,8 @@
 usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [--json out.json]
 
   kernel_us      per-kernel mean duration from the kernel trace of the bench
+  kernel_us_alone  the same over launches that overlap no other kernel (the
+                 serial event pass of a pipelined bench run)
                  command (trace/), and kernel_n the dispatch counts
   pmc            per-kernel, per-dispatch mean of every counter (pmc*/)
   traffic        HBM bytes per xa_decode_spec launch:
@@ -62,10 +64,25 @@ def main():
             bench = json.loads(lines[-1])
             out["bench"] = bench
     dur = defaultdict(list)
+    ks = []
     for r in rows(os.path.join(d, "trace", "**", "*kernel_trace.csv")):
-        dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        dur[short(r["Kernel_Name"])].append(b - a)
+        ks.append((a, b, short(r["Kernel_Name"])))
     out["kernel_us"] = {k: round(sum(v) / len(v) / 1e3, 2) for k, v in dur.items()}
     out["kernel_n"] = {k: len(v) for k, v in dur.items()}
+    # launches that share no time with any other kernel: with bench.py's
+    # --pipeline > 1 the timed steps overlap, and only the serial event pass
+    # (whose median is roofline.launch_ms) runs each kernel alone
+    ks.sort()
+    alone = defaultdict(list)
+    for i, (a, b, k) in enumerate(ks):
+        prev_end = max((e for _, e, _ in ks[:i]), default=0)
+        nxt = ks[i + 1][0] if i + 1 < len(ks) else b + 1
+        if prev_end <= a and nxt >= b:
+            alone[k].append(b - a)
+    out["kernel_us_alone"] = {k: round(sum(v) / len(v) / 1e3, 2) for k, v in alone.items()}
+    out["kernel_n_alone"] = {k: len(v) for k, v in alone.items()}
     out["pmc"] = counters(os.path.join(d, "pmc[0-9]*", "**", "*counter_collection.csv"))
     w0 = counters(os.path.join(d, "pmc_w0", "**", "*counter_collection.csv"))
     out["pmc_w0"] = w0
