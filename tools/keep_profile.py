@@ -37,6 +37,7 @@ def main():
               "read_bytes": t["read_bytes"], "write_bytes": t["write_bytes"],
               "bytes_per_rdreq": t["bytes_per_rdreq"],
               "spec_kernel_us_trace": summ["kernel_us"].get(summ["spec_key"]),
+              "spec_kernel_us_trace_alone": summ.get("kernel_us_alone", {}).get(summ["spec_key"]),
               "method": "write = WRITE_SIZE x 1 KiB; read = TCC_EA0_RDREQ x bytes per "
                         "request calibrated by a warm-up-0 pass (tools/pmc_summary.py)",
               "source": "profiles/%s_summary.json" % name}
