@@ -1,7 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-B="base=dbg/base/libbjxa.so.0 mnt=dbg/mnt/libbjxa.so.0 allnt=dbg/allnt/libbjxa.so.0"
-for wl in C3 C2 C5g C4; do
-timeout -k 10 300 python tools/ab_inproc.py --wl $wl --mix A --reps 4 --steps 20 $B > gpurun_out/aux_$wl.log 2>&1 || { echo "AB $wl failed"; tail -5 gpurun_out/aux_$wl.log; exit 1; }
-echo == $wl; grep -v amdgpu.ids gpurun_out/aux_$wl.log
-done
+bash tools/trace.sh c5 --workload C5 --steps 20 || exit 1
+bash tools/trace.sh c5n8 --workload C5 --streams 128 --steps 50 || exit 1
+bash tools/trace.sh c5n2 --workload C5 --streams 512 --steps 20 || exit 1
+for t in c5 c5n8 c5n2; do python3 tools/pmc_summary.py gpurun_out/prof_$t --json gpurun_out/prof_$t/summary.json > /dev/null; python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], {k: v for k, v in d["kernel_us_alone"].items() if "xa_" in k}, {k: v for k, v in d["kernel_us"].items() if "xa_" in k})' gpurun_out/prof_$t/summary.json; done
