@@ -28,7 +28,12 @@ other_configs.
 
 Reported:
   value       decoded MSamples/s of the whole job over the timed steps
-              (barrier + synchronize on both sides, max over ranks)
+              (barrier + synchronize on both sides, max over ranks); with
+              --pipeline D (default 2) consecutive steps run on D HIP
+              streams with their own output/workspace buffers, so one
+              step's tail overlaps the next step's head; every step is a
+              whole decode, and ms_per_step_serial times the same steps one
+              at a time
   roofline    the dominant kernel (xa_decode_spec; xa_decode_spec_batch for
               C5): algorithmic bytes per launch (XA read + PCM written,
               SURVEY.md §8(d): 3.03125 B per 8-bit sample) / its median
