@@ -1,7 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-L=bjxa_amd/libbjxa.so.0
-timeout -k 10 300 python tools/ab_inproc.py --wl C5g --mix A --reps 4 --steps 20 d=$L c192=$L:0:192 c256=$L:0:256 w4=$L:0:0:4 > gpurun_out/c5g_tune.log 2>&1 || { echo "AB failed"; tail -5 gpurun_out/c5g_tune.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/c5g_tune.log
-timeout -k 10 300 python tools/ab_inproc.py --wl C4 --mix A --reps 3 --steps 20 d=$L c256=$L:0:256 c320=$L:0:320 > gpurun_out/c4_tune.log 2>&1 || { echo "AB failed"; tail -5 gpurun_out/c4_tune.log; exit 1; }
-grep -v amdgpu.ids gpurun_out/c4_tune.log
+run() { tag=$1; shift; timeout -k 10 240 python bench.py --no-cpu --no-other --no-verify --workload C5 "$@" > gpurun_out/q_$tag.json 2> gpurun_out/q_$tag.err || { echo "FAILED $tag"; tail -5 gpurun_out/q_$tag.err; exit 1; }
+  python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d["ms_per_step"], d["ms_per_step_serial"], d["roofline"]["launch_ms"])' gpurun_out/q_$tag.json "$tag"; }
+for rep in 1 2; do
+for n in 512 256 128; do
+ for d in 1 2; do run n${n}_d${d}_$rep --streams $n --steps 40 --pipeline $d; done
+done
+done
