@@ -166,6 +166,15 @@ def reduce_over_ranks(elapsed, ok, dev):
     return float(t.item()), (bool(okt.item()) if ok is not None else None)
 
 
+def dist_on():
+    """True when this rank is in a process group (any world size): the
+    control-plane collectives then run through it, RCCL on the GPU box --
+    also at world size 1 under --force-pg, so that one GPU executes the
+    exact collectives the N > 1 line issues."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def job_value(samples_per_rank, world, steps, elapsed):
     """MSamples/s of a weak-scaling job: every rank decodes its own stream."""
     return samples_per_rank * world * steps / elapsed / 1e6
@@ -273,7 +282,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -281,7 +290,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
         step(i)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on():
         dist.barrier()
 
     serial = timed_serial(step, args.steps, dev) if len(slots) > 1 else elapsed
@@ -440,7 +449,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             for i in range(warmup):
                 step(i)
             torch.cuda.synchronize(dev)
-            if world > 1:
+            if dist_on():
                 dist.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -448,7 +457,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
                 step(i)
             torch.cuda.synchronize(dev)
             elapsed = time.perf_counter() - t0
-            if world > 1:
+            if dist_on():
                 dist.barrier()
             serial = timed_serial(step, steps, dev) if len(slots) > 1 else elapsed
             # kernel timing: slot 0 alone, one launch at a time
@@ -458,7 +467,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             spec = evs.ms()
             evs.close()
             torch.cuda.synchronize(dev)
-    elif world > 1:
+    elif dist_on():
         dist.barrier()
         dist.barrier()
     dsts, status = slots[0]["dsts"], slots[0]["status"]
@@ -595,6 +604,10 @@ def parse_args(argv=None):
     ap.add_argument("--pipeline", type=int, default=2,
                     help="steps in flight: consecutive steps on this many HIP streams, "
                          "each with its own output and workspace buffers")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="join an RCCL process group even at --gpus 1 (the rank starts "
+                         "under torch.distributed.run), so the control-plane collectives "
+                         "of the N > 1 line execute through librccl on one GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true",
@@ -604,7 +617,7 @@ def parse_args(argv=None):
 
 def main():
     args = parse_args()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.force_pg) and "WORLD_SIZE" not in os.environ:
         # the parent never touches the GPU: it only starts the ranks
         return launch_ranks(args.gpus)
 
@@ -637,7 +650,7 @@ def main():
                 dist.destroy_process_group()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.force_pg:
         dist.init_process_group("nccl", device_id=dev)
     workload = args.workload or ("C3" if world == 1 else "C5")
     try:
@@ -645,7 +658,7 @@ def main():
             return main_c5(args, dev, world, rank)
         return main_stream(args, workload, dev, world, rank)
     finally:
-        if world > 1:
+        if dist_on():
             dist.destroy_process_group()
 
 
@@ -664,7 +677,7 @@ def main_stream(args, workload, dev, world, rank):
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu
     r = run_workload(workload, args, dev, world, rank, not args.no_verify, cpu_leg)
     elapsed, ok = r["elapsed"], r["ok"]
-    if world > 1:
+    if dist_on():
         elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
 
     other = {}
@@ -744,7 +757,7 @@ def c5_control_plane(r, dev, world, nstreams):
     cnt = torch.tensor([r["samples"], r["alg_bytes"], r["repaired"], r["tail"], r["chunks"],
                         r["streams"]], dtype=torch.int64, device=dev)
     fe = torch.tensor([r["first_error"]], dtype=torch.int64, device=dev)
-    if world > 1:
+    if dist_on():
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
         dist.all_reduce(fe, op=dist.ReduceOp.MIN)
     width = (nstreams + world - 1) // world
@@ -755,7 +768,7 @@ def c5_control_plane(r, dev, world, nstreams):
         t[0] = len(vals)
         if vals:
             t[1:1 + len(vals)] = torch.tensor(vals, dtype=torch.int64)
-        if world == 1:
+        if not dist_on():
             return [t]
         parts = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(parts, t)
@@ -793,7 +806,7 @@ def main_c5(args, dev, world, rank, cdev=None):
     r = run_batch("C5", args.steps, args.warmup, dev, not args.no_verify, nstreams, rank,
                   world, args.eblocks, bad_stream=args.bad_stream, pipeline=args.pipeline)
     elapsed, ok = r["elapsed"], r["bit_exact"]
-    if world > 1:
+    if dist_on():
         elapsed, ok = reduce_over_ranks(elapsed, ok, cdev)
     job = c5_control_plane(r, cdev, world, nstreams)
     digest, match = checksum_report(job)
@@ -804,7 +817,7 @@ def main_c5(args, dev, world, rank, cdev=None):
     import torch.distributed as dist
     lm = torch.tensor([r["spec_ms"], r["frac"]], dtype=torch.float64, device=cdev)
     parts = [torch.zeros_like(lm) for _ in range(world)]
-    if world > 1:
+    if dist_on():
         dist.all_gather(parts, lm)
     else:
         parts = [lm]
@@ -847,7 +860,8 @@ def main_c5(args, dev, world, rank, cdev=None):
                           "repaired_chunks": job["repaired"], "tail_repairs": job["tail"],
                           "first_error_stream": None if job["first_error"] >= FIRST_ERR_NONE
                           else job["first_error"],
-                          "checksums_sha1": digest, "checksums_match_oracle": match},
+                          "checksums_sha1": digest, "checksums_match_oracle": match,
+                          "backend": dist.get_backend() if dist_on() else None},
     }
     if other:
         line["other_configs"] = other

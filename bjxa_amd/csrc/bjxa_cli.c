@@ -150,7 +150,10 @@ decode_stream(bjxa_decoder_t *dec, const bjxa_format_t *fmt, FILE *in,
 	if (got > 0 && bjxa_decode(dec, pcm, pcm_len, xa,
 	    (size_t)got * fmt->block_size_xa) != (int)got) {
 		const int e = errno;
-		good = first_bad_block(xa, got, fmt);
+		/* only a bad profile (EPROTO) leaves the PCM before it in the
+		 * buffer; any other failure (EIO, ENOMEM, ENODEV from the
+		 * device path) decoded nothing there, so nothing is written */
+		good = e == EPROTO ? first_bad_block(xa, got, fmt) : 0;
 		bad = 1;
 		errno = e;
 	}

@@ -118,7 +118,25 @@ read_all(void *buf, size_t n, FILE *file)
 #define OFFLOAD_ENCODE_DEFAULT	4096u
 
 static uint64_t offload_min[2];
+static int fault_gpu_decode;	/* BJXA_TEST_FAULT=gpu-decode (tests only) */
 static pthread_once_t offload_once = PTHREAD_ONCE_INIT;
+
+/* a threshold: decimal digits only, no sign, no blanks, no overflow */
+static int
+parse_threshold(const char *v, uint64_t *out)
+{
+	char *end;
+	unsigned long long n;
+
+	if (v == NULL || *v < '0' || *v > '9')
+		return (-1);
+	errno = 0;
+	n = strtoull(v, &end, 10);
+	if (errno == ERANGE || *end != '\0')
+		return (-1);
+	*out = (uint64_t)n;
+	return (0);
+}
 
 static void
 offload_init(void)
@@ -127,16 +145,26 @@ offload_init(void)
 	    "BJXA_OFFLOAD_ENCODE" };
 	const uint64_t dflt[2] = { OFFLOAD_DECODE_DEFAULT,
 	    OFFLOAD_ENCODE_DEFAULT };
+	const int saved = errno;
 
 	for (int d = 0; d < 2; d++) {
 		const char *v = getenv(env[d]);
-		char *end;
-		unsigned long long n = 0;
-		if (v != NULL && *v != '\0')
-			n = strtoull(v, &end, 10);
-		__atomic_store_n(&offload_min[d], (v != NULL && *v != '\0' &&
-		    *end == '\0') ? (uint64_t)n : dflt[d], __ATOMIC_RELAXED);
+		uint64_t n = dflt[d];
+		if (v != NULL && *v != '\0' && parse_threshold(v, &n) < 0) {
+			fprintf(stderr, "libbjxa: ignoring %s=\"%s\" (not a "
+			    "block count); using %llu\n", env[d], v,
+			    (unsigned long long)dflt[d]);
+			n = dflt[d];
+		}
+		__atomic_store_n(&offload_min[d], n, __ATOMIC_RELAXED);
 	}
+	/* fault injection for the CLI tests: a call routed to the device
+	 * fails with EIO before anything is decoded, with or without a GPU */
+	{
+		const char *f = getenv("BJXA_TEST_FAULT");
+		fault_gpu_decode = f != NULL && strcmp(f, "gpu-decode") == 0;
+	}
+	errno = saved;
 }
 
 static int
@@ -145,6 +173,15 @@ on_gpu(int dir, uint64_t eblocks)
 	(void)pthread_once(&offload_once, offload_init);
 	return eblocks >= __atomic_load_n(&offload_min[dir], __ATOMIC_RELAXED) &&
 	    bjxa__gpu_present();
+}
+
+/* BJXA_TEST_FAULT=gpu-decode and a call the threshold sends to the device */
+static int
+gpu_decode_faulted(uint64_t eblocks)
+{
+	(void)pthread_once(&offload_once, offload_init);
+	return fault_gpu_decode && eblocks >= __atomic_load_n(
+	    &offload_min[BJXA_HIP_OFFLOAD_DECODE], __ATOMIC_RELAXED);
 }
 
 int64_t
@@ -374,6 +411,8 @@ bjxa_decode(bjxa_decoder_t *dec, void *dst, size_t dst_len, const void *src,
 		copy = f->data_len_pcm;
 
 	memcpy(st, dec->state, sizeof st);
+	if (gpu_decode_faulted(n))
+		FAIL(EIO);
 	if (!on_gpu(BJXA_HIP_OFFLOAD_DECODE, n)) {
 		(void)bjxa__cpu_decode(src, (uint32_t)n, dec->bits,
 		    dec->channels, st, dst, copy, &err_cb);

@@ -49,10 +49,28 @@ struct xa_dec_args {
 	uint32_t *queue;	/* re-check queue, nchunks entries */
 	uint32_t *ctl;		/* XA_CTL_WORDS */
 	uint32_t *status;	/* XA_ST_WORDS */
+	uint32_t rep_C, rep_chunks;	/* reported as the status' chunk length
+					 * and count when nonzero (the region
+					 * kernel's K2 runs over regions) */
 };
 
 hipError_t xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
     unsigned variant, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+
+/*
+ * Region kernel (K1r, xa_decode.hip): lane chunks of XA_REGION_C(ch)
+ * eblocks with a warm-up of XA_REGION_W, 64 chunks per wave-region; `a.C`,
+ * `a.W` and `a.nchunks` describe the lane chunks, `a.g`/`a.e` need one entry
+ * per region (ceil(nchunks / 64)).  ncu: compute units of the device (the
+ * persistent grid).
+ */
+#define XA_REGION_C(ch)	((ch) == 2 ? 8u : 16u)
+#define XA_REGION_W	8u
+/* K2 alone (xa_decode.hip), over a.nchunks chunks of a.C eblocks */
+hipError_t xa_decode_fix_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
+    hipStream_t st);
+hipError_t xa_decode_region_launch(const xa_dec_args &a, unsigned bits,
+    unsigned ch, unsigned ncu, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 
 /*
  * Batched decode: many independent streams, mixed formats, one launch per

@@ -48,10 +48,7 @@
  * instructions (xa_step_lr), mono a single f32 chain (xa_step_f); both are
  * exact (xa_common.h).
  */
-#include <type_traits>
-
-#include "xa_common.h"
-#include "xa_decode.h"
+#include "xa_kern.h"
 
 #ifndef XA_SPEC_WPB
 #define XA_SPEC_WPB 4		/* waves per workgroup */
@@ -59,165 +56,7 @@
 #ifndef XA_FIX_PF
 #define XA_FIX_PF 4		/* repair windows in flight per lane */
 #endif
-#ifndef XA_DMA_AUX
-#define XA_DMA_AUX 0		/* cache policy bits of the input LDS-DMA */
-#endif
 
-/* ------------------------------------------------------------------ */
-
-__device__ __forceinline__ void
-wave_lds_sync()
-{
-	/* LDS ops of one wave complete in order; stop the compiler moving
-	 * them across this point */
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-/* compile-time loop: f(integral_constant<int, I>) for I in [I, N) */
-template <int I, int N> struct sfor {
-	template <typename F>
-	__device__ __forceinline__ static void run(F &f)
-	{
-		f(std::integral_constant<int, I>());
-		sfor<I + 1, N>::run(f);
-	}
-};
-template <int N> struct sfor<N, N> {
-	template <typename F>
-	__device__ __forceinline__ static void run(F &) {}
-};
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
-typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(16)));
-#define LDS_PTR(p) ((__attribute__((address_space(3))) void *)(p))
-
-/* block geometry, all compile-time */
-template <int BITS, int CH> struct geo {
-	static constexpr int BSZ = BITS * 4 + 1;	/* channel block */
-	static constexpr int EBSZ = BSZ * CH;		/* effective block */
-	static constexpr int G = 4 / CH;		/* eblocks per group */
-	static constexpr int G2 = XA_CHUNK_Q(CH);	/* chunk granularity */
-	static constexpr int GDW = BSZ;			/* dwords per group */
-	static constexpr int OB = 64 * CH;		/* PCM bytes per eblock */
-};
-
-/* first eblock of chunk q (chunks [0, nlong) are G longer; G = G2) */
-template <int G>
-__device__ __forceinline__ int64_t
-chunk_start(const xa_dec_args &a, uint32_t q)
-{
-	return (int64_t)q * a.C + (int64_t)G * min(q, a.nlong);
-}
-
-/*
- * Decode the channel blocks of one eblock whose first byte is byte O of w,
- * advancing the lane's state.  With STORE the output goes to `line` in
- * 16-B pieces, numbered from QB (the eblock's first piece within the
- * group); after every LB bytes `flush(h)` runs (h = LB-byte line index
- * within the group), and with RESTART the next line is written at `line`
- * again (LDS staging), otherwise output continues at line + LB (direct
- * stores).  A line may span eblocks (mono: 64 B per block).  Returns a bit
- * per channel whose gain nibble is >= 5.
- */
-template <int BITS, int CH, bool STORE, bool RESTART, int LB, int QB = 0,
-    typename F>
-__device__ __forceinline__ uint32_t
-decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
-    uint8_t *line, F &flush)
-{
-	constexpr int BSZ = BITS * 4 + 1;
-	uint32_t sh[CH], bad = 0;
-	int32_t k0[CH], k1[CH];
-#pragma unroll
-	for (int c = 0; c < CH; c++) {
-		const int pb = O + c * BSZ;
-		uint32_t prof = (w[pb >> 2] >> (8 * (pb & 3))) & 0xffu;
-		uint32_t gain = prof >> 4;
-		sh[c] = 16u + (prof & 15u);
-		xa_gain(gain & 7u, k0[c], k1[c]);
-		bad |= (gain >= 5u) ? (1u << c) : 0u;
-	}
-	/* f32 state for the block (xa_common.h): stereo runs both chains in
-	 * one packed instruction stream (xa_step_lr), mono one chain
-	 * (xa_step_f); the int state converts in and out once per eblock.
-	 * shp: the range of each half of a packed code pair (mono: both
-	 * halves are the block's one range) */
-	xa_f2 f0 = {(float)p0[0], (float)p0[CH - 1]};
-	xa_f2 f1 = {(float)p1[0], (float)p1[CH - 1]};
-	const xa_f2 fk0 = xa_f2{(float)k0[0], (float)k0[CH - 1]} * (1.0f / 256.0f);
-	const xa_f2 fk1 = xa_f2{(float)k1[0], (float)k1[CH - 1]} * (1.0f / 256.0f);
-	const uint32_t shp = (sh[0] - 16u) | ((sh[CH - 1] - 16u) << 16);
-	float m0 = f0.x, m1 = f1.x;	/* mono state */
-	/* 16-B piece q holds 4 stereo frames or 8 mono samples */
-#pragma unroll
-	for (int q = 0; q < 4 * CH; q++) {
-		uint32_t fr[4];
-#pragma unroll
-		for (int j = 0; j < 4; j++) {
-			if (CH == 2) {
-				const int n = 4 * q + j;
-				uint32_t tp;
-				if (BITS == 8) {
-					/* code n of L -> bits 8..15, of R -> 24..31 */
-					const int bl = O + 1 + n, br = O + BSZ + 1 + n;
-					tp = __builtin_amdgcn_perm(w[br >> 2], w[bl >> 2],
-					    0x000c000cu | (uint32_t)(bl & 3) << 8 |
-					    (uint32_t)(4 + (br & 3)) << 24);
-				} else {
-					tp = __builtin_amdgcn_perm(
-					    (uint32_t)code_at<BITS>(w, O + BSZ, n),
-					    (uint32_t)code_at<BITS>(w, O, n), 0x07060302u);
-				}
-				fr[j] = xa_step_lr(xa_pk_ashr(tp, shp), fk0, fk1, f0, f1);
-			} else {
-				/* codes n, n+1 into the halves, one packed shift */
-				const int n = 8 * q + 2 * j;
-				uint32_t tp;
-				if (BITS == 8) {
-					const int b = O + 1 + n;
-					tp = __builtin_amdgcn_perm(w[(b + 1) >> 2],
-					    w[b >> 2], 0x000c000cu |
-					    (uint32_t)(b & 3) << 8 |
-					    (uint32_t)(((b + 1) >> 2) == (b >> 2) ?
-					    (b + 1) & 3 : 4 + ((b + 1) & 3)) << 24);
-				} else {
-					tp = __builtin_amdgcn_perm(
-					    (uint32_t)code_at<BITS>(w, O, n + 1),
-					    (uint32_t)code_at<BITS>(w, O, n), 0x07060302u);
-				}
-				const uint32_t t = xa_pk_ashr(tp, shp);
-				int32_t sa = xa_step_f<false>(t, fk0.x, fk1.x, m0, m1);
-				int32_t sb = xa_step_f<true>(t, fk0.x, fk1.x, m0, m1);
-				fr[j] = __builtin_amdgcn_perm((uint32_t)sb,
-				    (uint32_t)sa, 0x05040100u);
-			}
-		}
-		if (STORE) {
-			u32x4a v = { fr[0], fr[1], fr[2], fr[3] };
-			constexpr int QL = LB / 16;	/* pieces per line */
-			const int qq = QB + q;
-			*(u32x4a *)(line + 16 * (RESTART ? (qq % QL) : qq)) = v;
-			if (qq % QL == QL - 1)
-				flush(qq / QL);
-		}
-		/* keep the unpack of later codes from being hoisted here: it
-		 * would only raise register pressure */
-		__builtin_amdgcn_sched_barrier(0);
-	}
-	if (CH == 1) {
-		p0[0] = (int32_t)m0;
-		p1[0] = (int32_t)m1;
-	}
-	if (CH == 2) {
-		p0[0] = (int32_t)f0.x;
-		p0[CH - 1] = (int32_t)f0.y;
-		p1[0] = (int32_t)f1.x;
-		p1[CH - 1] = (int32_t)f1.y;
-	}
-	return bad;
-}
 
 /*
  * Store the wave's staged LB-byte lines: line j belongs to chunk
@@ -316,19 +155,6 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 	}
 }
 
-/* one LDS-DMA instruction of PS bytes per lane (the builtin wants a
- * literal size) */
-template <int PS> __device__ __forceinline__ void dma(const void *, uint8_t *);
-template <> __device__ __forceinline__ void
-dma<4>(const void *g, uint8_t *l)
-{
-	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 4, 0, XA_DMA_AUX);
-}
-template <> __device__ __forceinline__ void
-dma<16>(const void *g, uint8_t *l)
-{
-	__builtin_amdgcn_global_load_lds(g, LDS_PTR(l), 16, 0, XA_DMA_AUX);
-}
 
 /*
  * K1.  One lane per chunk, XA_SPEC_WPB waves per workgroup.
@@ -906,8 +732,8 @@ drain_tail(const xa_dec_args &a)
 	a.status[XA_ST_STATE_R] = fin.y;
 	a.status[XA_ST_FIXED] = a.ctl[XA_CTL_FIXED];
 	a.status[XA_ST_TAIL] = tail;
-	a.status[XA_ST_CHUNKS] = a.nchunks;
-	a.status[XA_ST_C] = a.C;
+	a.status[XA_ST_CHUNKS] = a.rep_chunks ? a.rep_chunks : a.nchunks;
+	a.status[XA_ST_C] = a.rep_C ? a.rep_C : a.C;
 	a.status[XA_ST_W] = a.W;
 	a.ctl[XA_CTL_ERR] = 0xffffffffu;
 	a.ctl[XA_CTL_NQ] = 0;
@@ -1027,6 +853,48 @@ xa_decode_fix(xa_dec_args a)
 
 /* ------------------------------------------------------------------ */
 
+/* K2 over a.nchunks chunks of a.C eblocks */
+template <int BITS, int CH>
+static hipError_t
+fix_launch(const xa_dec_args &a, hipStream_t st)
+{
+	unsigned grid2 = (a.nchunks + 256u * XA_FIX_CPT - 1) / (256u * XA_FIX_CPT);
+	if (grid2 > 256u)
+		grid2 = 256u;
+#ifdef XA_FIX_NOBUF
+	const bool buf = false;
+#else
+	/* buffer-descriptor windows need 32-bit byte offsets */
+	const bool buf = (uint64_t)a.eblocks * geo<BITS, CH>::EBSZ <
+	    (1ull << 32) - 256u;
+#endif
+	if (buf)
+		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, true>), dim3(grid2),
+		    dim3(256), 0, st, a);
+	else
+		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, false>), dim3(grid2),
+		    dim3(256), 0, st, a);
+	return hipGetLastError();
+}
+
+hipError_t
+xa_decode_fix_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
+    hipStream_t st)
+{
+	if (ch == 1) {
+		if (bits == 8)
+			return fix_launch<8, 1>(a, st);
+		if (bits == 6)
+			return fix_launch<6, 1>(a, st);
+		return fix_launch<4, 1>(a, st);
+	}
+	if (bits == 8)
+		return fix_launch<8, 2>(a, st);
+	if (bits == 6)
+		return fix_launch<6, 2>(a, st);
+	return fix_launch<4, 2>(a, st);
+}
+
 template <int BITS, int CH>
 static hipError_t
 launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
@@ -1057,19 +925,9 @@ launch(const xa_dec_args &a, unsigned variant, hipStream_t st, hipEvent_t ev0,
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
 #if !defined(XA_DBG_STEP) && !defined(XA_DBG_NOSTORE) && !defined(XA_DBG_CONTIG)
-#ifdef XA_FIX_NOBUF
-	const bool buf = false;
-#else
-	/* buffer-descriptor windows need 32-bit byte offsets */
-	const bool buf = (uint64_t)a.eblocks * geo<BITS, CH>::EBSZ <
-	    (1ull << 32) - 256u;
-#endif
-	if (buf)
-		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, true>), dim3(grid2),
-		    dim3(256), 0, st, a);
-	else
-		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, false>), dim3(grid2),
-		    dim3(256), 0, st, a);
+	const hipError_t e2 = fix_launch<BITS, CH>(a, st);
+	if (e2 != hipSuccess)
+		return e2;
 #endif
 	return hipGetLastError();
 }
@@ -1139,6 +997,7 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.W = b.W;
 	a.nlong = 0;
 	a.pace = 0;	/* the batch kernel decides per workgroup */
+	a.rep_C = a.rep_chunks = 0;
 	a.init[0] = d.init[0];
 	a.init[1] = d.init[1];
 	a.g = b.g + d.cbase;

@@ -31,6 +31,8 @@
 #define MAX_DEVICES	64
 #define XA_VARIANT_STRUCT	0xfu	/* kernel structure, 0 = automatic */
 #define XA_VARIANT_BALANCED	0x20u	/* two-length chunk plan */
+#define XA_VARIANT_STRIDED	0x40u	/* the lane-strided K1 instead of K1r */
+#define XA_VARIANT_REGION	0x80u	/* K1r (experimental, opt-in) */
 
 /* a HIP device is visible; probed once per process, thread-safe */
 extern "C" int
@@ -76,7 +78,26 @@ struct plan {
 	uint32_t	C, W;		/* base chunk and warm-up, eblocks */
 	uint32_t	nlong;		/* leading chunks that are C + G long */
 	uint32_t	nchunks;
+	uint32_t	nstate;		/* entries of the g/e arrays (K2's chunks) */
+	bool		region;		/* the region kernel (K1r) */
 };
+
+/*
+ * The region kernel (K1r, xa_decode.hip) is the automatic choice: fixed lane
+ * chunks (XA_REGION_C) and warm-up (XA_REGION_W), K2 over regions of 64
+ * chunks.  An explicit chunk or warm-up, the two-length plan, a kernel
+ * structure (variant bits 0-3) or XA_VARIANT_STRIDED select the
+ * lane-strided K1.
+ */
+static bool
+use_region(const bjxa_hip_tuning_t *t)
+{
+	if (t == NULL || !(t->variant & XA_VARIANT_REGION))
+		return false;
+	return t->chunk == 0 && (t->warmup < 0 || (uint32_t)t->warmup == XA_REGION_W) &&
+	    (t->variant & (XA_VARIANT_STRUCT | XA_VARIANT_BALANCED |
+	    XA_VARIANT_STRIDED)) == 0;
+}
 
 /*
  * Chunk plan for one stream.  Automatic: uniform chunks (above).  With
@@ -94,6 +115,15 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 	const uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup :
 	    DEFAULT_WARMUP;
 	uint32_t c;
+	p->region = use_region(t);
+	if (p->region) {
+		p->C = XA_REGION_C(ch);
+		p->W = XA_REGION_W;
+		p->nlong = 0;
+		p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
+		p->nstate = (p->nchunks + 63u) / 64u;
+		return;
+	}
 	p->W = round_up(w, G);
 	p->nlong = 0;
 	if (t && t->chunk) {
@@ -118,12 +148,14 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 			else
 				p->nchunks = nl + (uint32_t)((eblocks - cover +
 				    c - 1) / c);
+			p->nstate = p->nchunks;
 			return;
 		}
 		c = MIN_CHUNK;
 	}
 	p->C = round_up(c, G);
 	p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
+	p->nstate = p->nchunks;
 }
 
 /*
@@ -176,7 +208,7 @@ bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
 	if (channels != 1 && channels != 2)
 		return 0;
 	plan_chunks(eblocks, channels, tune, &p);
-	return ws_bytes(p.nchunks);
+	return ws_bytes(p.nstate);
 }
 
 __global__ void
@@ -240,20 +272,25 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	    ((uint32_t)(uint16_t)s->state[1] << 16);
 	a.init[1] = ((uint32_t)(uint16_t)s->state[2]) |
 	    ((uint32_t)(uint16_t)s->state[3] << 16);
-	if (ws_len < ws_bytes(a.nchunks)) {
+	a.rep_C = a.rep_chunks = 0;
+	if (ws_len < ws_bytes(p.nstate)) {
 		errno = EINVAL;
 		return -1;
 	}
 	uint8_t *ws = (uint8_t *)d_ws;
 	a.ctl = (uint32_t *)ws;
 	a.g = (uint2 *)(ws + XA_CTL_WORDS * 4);
-	a.e = a.g + a.nchunks;
-	a.queue = (uint32_t *)(a.e + a.nchunks);
+	a.e = a.g + p.nstate;
+	a.queue = (uint32_t *)(a.e + p.nstate);
 	a.status = d_status;
-	if (xa_decode_launch(a, s->bits, s->channels, pick_variant(s->channels, tune),
-	    (hipStream_t)stream,
-	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
-	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
+	hipEvent_t e0 = tune ? (hipEvent_t)tune->ev_spec[0] : NULL;
+	hipEvent_t e1 = tune ? (hipEvent_t)tune->ev_spec[1] : NULL;
+	const hipError_t rc = p.region ?
+	    xa_decode_region_launch(a, s->bits, s->channels, target_lanes() / 512u,
+	    (hipStream_t)stream, e0, e1) :
+	    xa_decode_launch(a, s->bits, s->channels, pick_variant(s->channels, tune),
+	    (hipStream_t)stream, e0, e1);
+	if (rc != hipSuccess) {
 		errno = EIO;
 		return -1;
 	}

@@ -264,3 +264,49 @@ def test_sub_block_stream(cli):
         assert rc == 0, err
         want, _, _ = expected_decode(xa)
         assert out == want
+
+
+@pytest.mark.parametrize("route", ROUTES)
+@pytest.mark.parametrize("shape", ["stream", "blocks"])
+def test_decode_device_failure_writes_no_pcm(cli, golden, shape, route):
+    """A decode call that fails for any reason other than a bad profile
+    (here EIO, injected by BJXA_TEST_FAULT on every call the offload
+    threshold sends to the device) leaves nothing decoded in the buffer:
+    the CLI writes the RIFF header and no PCM, then the error (ADVICE r02:
+    never PCM of a failed call)."""
+    data = golden("square-stereo-8.xa")
+    env = route_env(route, shape)
+    env["BJXA_TEST_FAULT"] = "gpu-decode"
+    if route == "cpu":
+        env["BJXA_OFFLOAD_DECODE"] = "1"
+    rc, out, err = run(["decode"], data, env=env)
+    assert rc != 0 and "bjxa_decode: Input/output error" in err
+    want, _, _ = expected_decode(data)
+    assert out == want[:44]
+
+
+@pytest.mark.parametrize("value", ["-1", " 5", "+5", "12x", "99999999999999999999999", ""])
+def test_offload_threshold_env_rejects_bad_values(built, value):
+    """BJXA_OFFLOAD_DECODE must be a plain decimal block count: a sign,
+    blanks, junk or an overflowing value fall back to the default (1024)
+    with one warning instead of wrapping to 'never offload'."""
+    import subprocess
+    import sys
+    code = ("import bjxa_amd; print(bjxa_amd.offload_threshold(0), "
+            "bjxa_amd.offload_threshold(1))")
+    env = dict(os.environ, BJXA_OFFLOAD_DECODE=value, **no_gpu())
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       env=env, cwd=ROOT, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.split() == ["1024", "4096"]
+    assert ("ignoring BJXA_OFFLOAD_DECODE" in p.stderr) == (value != "")
+
+
+def test_offload_threshold_env_accepts_count(built):
+    import subprocess
+    import sys
+    code = "import bjxa_amd; print(bjxa_amd.offload_threshold(0))"
+    env = dict(os.environ, BJXA_OFFLOAD_DECODE="77", **no_gpu())
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       env=env, cwd=ROOT, timeout=120)
+    assert p.returncode == 0 and p.stdout.split() == ["77"] and p.stderr == ""
