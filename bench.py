@@ -30,7 +30,8 @@ Reported:
   value       decoded MSamples/s of the whole job over the timed steps
               (barrier + synchronize on both sides, max over ranks); with
               --pipeline D (default 2) consecutive steps run on D HIP
-              streams with their own output/workspace buffers, so one
+              streams with their own input copy and output/workspace
+              buffers (no slot can hit another's input in a cache), so one
               step's tail overlaps the next step's head; every step is a
               whole decode, and ms_per_step_serial times the same steps one
               at a time
@@ -45,9 +46,9 @@ Reported:
   cpu_baseline  rank 0 at N = 1, for every line: the oracle (CPU
               restatement of libbjxa's decode/encode): C2/C3 and the encode on
               1 thread (a stream is serial), C4/C5/C5g on all host cores the
-              process may use (capped at 16, the box's share), one decoder
-              per thread, streams round-robin; median of 5 passes after a
-              discarded first
+              process may use (its affinity mask; BJXA_CPU_THREADS lowers
+              it), one decoder per thread, streams round-robin; median of 5
+              passes after a discarded first
 
 CPU rehearsal: BJXA_BENCH_BACKEND=gloo runs the N > 1 path on CPU (gloo,
 small job via --streams/--eblocks), decoding each rank's share with the
@@ -88,7 +89,6 @@ METRIC = "decoded PCM MSamples/s (+ achieved HBM GB/s vs roofline), bit-exact vs
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 CPU_PASSES = 5
 EV_SAMPLES = 20         # launches timed with events, after the timed region
-CPU_THREADS_CAP = 16    # a GPU box's CPU share per GPU
 NO_ERROR = 0xFFFFFFFF
 FIRST_ERR_NONE = (1 << 62)
 
@@ -192,12 +192,19 @@ def host_cpu():
 
 
 def cpu_threads():
-    """Host cores this process may use, capped at the box's per-GPU share."""
+    """Threads for the batch CPU baseline: every core in this process's
+    affinity mask (BASELINE.md "all online host cores"), unless
+    BJXA_CPU_THREADS lowers it (a shared box's per-GPU share).  Returns
+    (threads, cores in the affinity mask, CPUs online)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(n, CPU_THREADS_CAP)), os.cpu_count()
+        aff = os.cpu_count() or 1
+    n = aff
+    cap = os.environ.get("BJXA_CPU_THREADS", "")
+    if cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n), aff, os.cpu_count()
 
 
 # ---- PCM checksums (the AllGather payload) -------------------------------------
@@ -239,12 +246,14 @@ def pipeline_slots(depth, dev, make):
     go to consecutive slots, so step i+1's spec kernel can take the CUs that
     step i's tail leaves idle and step i's verify/repair kernel runs beside
     it; step i+depth reuses slot i's buffers after step i on the same
-    stream.  Every step is still a whole decode of its batch."""
+    stream.  Every step is still a whole decode of its batch.  make(k)
+    builds slot k's buffers (slots k >= 1 copy the input, so no step reads
+    another slot's input out of a cache)."""
     import torch
     slots = []
     for k in range(max(1, depth)):
         st = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
-        sl = make()
+        sl = make(k)
         sl["stream"] = st
         sl["sh"] = st.cuda_stream
         slots.append(sl)
@@ -265,7 +274,8 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     xa_np = synth.stream(eb, bits, ch, args.mix, seed=rank)
     src = torch.from_numpy(xa_np).to(dev)
     ws_len = bjxa_amd.decode_workspace_size(eb, ch, args.chunk, args.warm_blocks)
-    slots = pipeline_slots(args.pipeline, dev, lambda: {
+    slots = pipeline_slots(args.pipeline, dev, lambda k: {
+        "src": src if k == 0 else src.clone(),
         "dst": torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev),
         "ws": torch.zeros(ws_len, dtype=torch.uint8, device=dev),
         "status": torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device=dev)})
@@ -275,7 +285,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
 
     def step(i, ev=(None, None)):
         sl = slots[i % len(slots)]
-        bjxa_amd.decode_device(src.data_ptr(), sl["dst"].data_ptr(), eb, eb * 32, bits, ch,
+        bjxa_amd.decode_device(sl["src"].data_ptr(), sl["dst"].data_ptr(), eb, eb * 32, bits, ch,
                                sl["ws"].data_ptr(), ws_len, sl["status"].data_ptr(),
                                (0, 0, 0, 0), args.chunk, args.warm_blocks, sl["sh"], ev)
 
@@ -324,7 +334,13 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
                    "kind": "port",
                    "sample": "the full %s stream (%d samples), oracle/xa_oracle.c single-pass "
                              "decode on 1 thread, median of %d passes after a discarded first; "
-                             "host CPU: %s" % (name, samples, CPU_PASSES, host_cpu())}
+                             "host CPU: %s" % (name, samples, CPU_PASSES, host_cpu()),
+                   "why": "libbjxa's CPU path cannot be built here (its autoconf config.h is "
+                          "absent), so the baseline is oracle/xa_oracle.c, which restates "
+                          "its loop shape for shape (bjxa_decode -> inflate -> "
+                          "decode_inflated, src/libbjxa.c:602-661, :286-345, :533-578); "
+                          "product_cpu_core is this library's own faster CPU path",
+                   "product_cpu_core": product_cpu_core(xa_np, eb, bits, ch)}
         del ref
 
     xa_bytes = eb * ch * (bits * 4 + 1)
@@ -333,6 +349,31 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
             "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
             "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
+
+
+def product_cpu_core(xa_np, eb, bits, ch, sample_eb=1_000_000):
+    """This library's own CPU core (bjxa_decode routed off the GPU,
+    bjxa_amd/csrc/xa_cpu.c) on the first `sample_eb` eblocks of the stream,
+    1 thread, median of 3 passes after a discarded first."""
+    import bjxa_amd
+    n = min(eb, sample_eb)
+    bsz = (bits * 4 + 1) * ch
+    xa = np.ascontiguousarray(xa_np[:n * bsz])
+    pcm = np.zeros(n * 32 * ch, np.int16)
+    times = []
+    with bjxa_amd.offload(None):
+        for k in range(4):
+            with bjxa_amd.Decoder() as d:
+                d.parse_header(bjxa_amd.xa_header(xa.size, n * 32, 44100, bits, ch))
+                t = time.perf_counter()
+                d.decode(pcm, xa)
+                if k:
+                    times.append(time.perf_counter() - t)
+    med = float(np.median(times))
+    return {"value": round(n * 32 * ch / med / 1e6, 1), "unit": "MSamples/s", "cores": 1,
+            "sample": "first %d eblocks (%d samples) through bjxa_decode() on the library's "
+                      "CPU core (bjxa_amd/csrc/xa_cpu.c), median of 3 passes after a "
+                      "discarded first" % (n, n * 32 * ch)}
 
 
 # ---- batched streams (C4/C5) ------------------------------------------------
@@ -390,17 +431,21 @@ def oracle_batch(inputs, threads):
 
 def cpu_batch_baseline(name, inputs):
     """C4/C5 CPU baseline: the oracle on all usable host cores."""
-    threads, online = cpu_threads()
+    threads, aff, online = cpu_threads()
     samples = sum(eb * 32 * ch for _, _, ch, eb, _ in inputs)
     oracle_batch(inputs, threads)                       # discarded first pass
     times = [oracle_batch(inputs, threads)[1] for _ in range(CPU_PASSES)]
     med = float(np.median(times))
     return {"value": round(samples / med / 1e6, 1), "unit": "MSamples/s", "cores": threads,
-            "kind": "port",
-            "sample": "all %d streams of %s (%d samples), oracle/xa_oracle.c single-pass decode, "
-                      "one decoder per thread on %d threads, streams round-robin, median of %d "
-                      "passes after a discarded first; host: %s, %s CPUs online"
-                      % (len(inputs), name, samples, threads, CPU_PASSES, host_cpu(), online)}
+            "cores_affinity": aff, "cpus_online": online, "kind": "port",
+            "sample": "all %d streams of %s (%d samples), oracle/xa_oracle.c single-pass decode "
+                      "(libbjxa's block loop restated, src/libbjxa.c:602-661), one decoder per "
+                      "thread on %d threads (%d cores in the affinity mask%s), streams "
+                      "round-robin, median of %d passes after a discarded first; host: %s, "
+                      "%s CPUs online"
+                      % (len(inputs), name, samples, threads, aff,
+                         "; BJXA_CPU_THREADS" if threads < aff else "", CPU_PASSES,
+                         host_cpu(), online)}
 
 
 def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, eblocks=0,
@@ -426,10 +471,12 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
     alg = sum(xa.nbytes + eb * 64 * ch for _, _, ch, eb, xa in inputs)
     n = len(inputs)
 
-    def make_slot():
+    def make_slot(k):
         dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev)
                 for _, _, ch, eb, _ in inputs]
-        return {"dsts": dsts,
+        # slot 0 decodes the callers' inputs, every other slot its own copy
+        own = srcs if k == 0 else [s.clone() for s in srcs]
+        return {"dsts": dsts, "srcs": own,
                 "status": torch.zeros(max(n, 1) * bjxa_amd.STATUS_WORDS, dtype=torch.int32,
                                       device=dev)}
     slots = pipeline_slots(pipeline, dev, make_slot)
@@ -439,7 +486,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             for sl in slots:
                 desc = [{"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
                          "bits": bits, "channels": ch}
-                        for s, d, (_, bits, ch, eb, _) in zip(srcs, sl["dsts"], inputs)]
+                        for s, d, (_, bits, ch, eb, _) in zip(sl["srcs"], sl["dsts"], inputs)]
                 sl["batch"] = stack.enter_context(bjxa_amd.Batch(desc, stream=sl["sh"]))
             torch.cuda.synchronize(dev)
 
@@ -483,7 +530,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
                     default=FIRST_ERR_NONE)
     ok, ref_sums = None, None
     if verify:
-        threads, _ = cpu_threads()
+        threads = cpu_threads()[0]
         refs, _ = oracle_batch(inputs, max(1, threads // world))
         ok, ref_sums = same, []
         for (i, bits, ch, eb, xa), d, w in zip(inputs, dsts, st):
@@ -532,15 +579,21 @@ def run_encode(steps, warmup, dev, verify, cpu_leg=False):
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
     # per-launch kernel time: events around each of EV_SAMPLES launches
-    # (encode is one kernel, so torch's events on the same stream suffice)
+    # (encode is one kernel, so torch's events on the same stream suffice),
+    # each launch after a 512 MiB fill that evicts the 256 MiB Infinity
+    # Cache, so no launch reads its 640 MB input partly from the cache
+    # (round-2 VERDICT: an isolated launch otherwise times below the trace)
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
     ms = []
-    for _ in range(max(EV_SAMPLES, steps)):
+    for i in range(max(EV_SAMPLES, steps)):
+        flush.fill_(i & 255)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
         e1.record()
         e1.synchronize()
         ms.append(e0.elapsed_time(e1))
+    del flush
     med = float(np.median(ms))
     ok, cpu = None, None
     if verify or cpu_leg:
@@ -553,8 +606,10 @@ def run_encode(steps, warmup, dev, verify, cpu_leg=False):
                 t = time.perf_counter()
                 oracle.encode(pcm, frames, bits, ch)
                 times.append(time.perf_counter() - t)
-            med = float(np.median(times))
-            cpu = {"value": round(frames * ch / med / 1e6, 1), "unit": "MSamples/s",
+            # (its own name: this median once overwrote the kernel's, so
+            # round 2's encode kernel_ms was the CPU time in seconds)
+            cpu_s = float(np.median(times))
+            cpu = {"value": round(frames * ch / cpu_s / 1e6, 1), "unit": "MSamples/s",
                    "cores": 1, "kind": "port",
                    "sample": "the full C3-shaped PCM (%d samples), oracle/xa_oracle.c "
                              "single-pass encode on 1 thread, median of %d passes after a "
@@ -566,7 +621,10 @@ def run_encode(steps, warmup, dev, verify, cpu_leg=False):
             "value": round(frames * ch / dt / 1e6, 1), "unit": "MSamples/s",
             "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(med, 4),
             "kernel_samples": len(ms),
-            "frac": round(alg / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
+            "kernel_ms_stat": "median of %d launches, each after a 512 MiB cache-evicting "
+                              "fill" % len(ms),
+            "frac": round(alg / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_frac": round(alg / dt / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
             "byte_exact": ok, "cpu_baseline": cpu}
 
 
@@ -633,7 +691,7 @@ def main():
         return 2
     if backend == "gloo":
         dev = torch.device("cpu")
-        if world > 1:
+        if world > 1 or args.force_pg:
             dist.init_process_group("gloo")
         return main_c5_cpu(args, dev, world, rank)
     if backend == "gloo-gpu":
@@ -884,7 +942,7 @@ def main_c5_cpu(args, dev, world, rank):
     specs = batch_specs("C5", nstreams, eblocks)
     lo, hi = shard_range(len(specs), rank, world)
     inputs = batch_inputs("C5", nstreams, eblocks, lo, hi, args.bad_stream)
-    if world > 1:
+    if dist_on():
         dist.barrier()
     t0 = time.perf_counter()
     first_err, pcms = FIRST_ERR_NONE, {}
@@ -910,7 +968,7 @@ def main_c5_cpu(args, dev, world, rank):
         ref, _ = oracle_batch(inputs, 1)
         refs = [pcm_checksum_np(ref[i][0][:ref[i][2] * 32 * ch]) for i, bits, ch, eb, xa in inputs]
         ok = sums == refs
-    if world > 1:
+    if dist_on():
         elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
     samples = sum(eb * 32 * ch for _, _, ch, eb, _ in inputs)
     r = {"samples": samples, "alg_bytes": 0, "repaired": 0, "tail": 0, "chunks": 0,
@@ -926,6 +984,7 @@ def main_c5_cpu(args, dev, world, rank):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "int32", "data": "synthetic (seeded XA streams, profile mix A)",
             "device": "cpu (gloo rehearsal of the RCCL path; library host API on its CPU core)",
+            "backend": dist.get_backend() if dist_on() else None,
             "config": {"workload": "C5-shaped: %d streams of %d eblocks" % (nstreams, eblocks),
                        "workload_id": "C5", "streams": job["streams"],
                        "streams_per_rank": [b - a for a, b in job["shards"]]},
@@ -936,7 +995,7 @@ def main_c5_cpu(args, dev, world, rank):
                               "checksums_sha1": digest, "checksums_match_oracle": match}}
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on():
         dist.destroy_process_group()
     return 0 if ok in (None, True) else 1
 

@@ -127,19 +127,34 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
         f = device_bytes(dst + off, 4 * ch).view(np.int16).reshape(2, ch)
         return {c: (int(f[1][c]), int(f[0][c])) for c in chans}
 
+    keep = []      # full-block scratch PCM of a cut last block, alive while used
+
     def run(first, state):
+        """Decode [first, hi) from `state`.  Always whole blocks (as
+        bjxa__gpu_decode does): when the stream's last block is cut, the
+        range decodes into a full-block scratch buffer and only the
+        stream's frames are copied to the caller's PCM, so frames 30/31 of
+        every block -- the carried state of a bad right block in the last
+        eblock included -- are real (round-2 ADVICE)."""
         n = hi - first
         fr = min(frames, hi * 32) - first * 32
         src = d_src_range + (first - w0) * ebsz
         dst = d_dst_range + (first - w0) * 64 * ch
+        out = dst
+        if fr < n * 32:
+            full = torch.empty(n * 64 * ch, dtype=torch.uint8, device="cuda")
+            keep.append(full)
+            out = full.data_ptr()
         ws_len = bjxa_amd.decode_workspace_size(n, ch)
         ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
         st = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
         bjxa_amd.workspace_init(ws.data_ptr(), ws_len, stream)
-        bjxa_amd.decode_device(src, dst, n, fr, bits, ch, ws.data_ptr(), ws_len,
+        bjxa_amd.decode_device(src, out, n, n * 32, bits, ch, ws.data_ptr(), ws_len,
                                st.data_ptr(), state, stream=stream)
         torch.cuda.synchronize()
-        return dst, st.cpu().numpy().view(np.uint32).copy()
+        if out != dst:
+            device_copy(dst, out, fr * 2 * ch)
+        return out, st.cpu().numpy().view(np.uint32).copy()
 
     def decode(first, state):
         dst, words = run(first, state)
@@ -169,6 +184,15 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
         return at_lo, out, j * ch + bad_c
 
     return decode
+
+
+def device_copy(d_to, d_from, nbytes):
+    """hipMemcpy device to device (synchronous)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    if nbytes and hip.hipMemcpy(d_to, d_from, nbytes, 3) != 0:
+        raise RuntimeError("hipMemcpy failed")
 
 
 def device_bytes(d_ptr, nbytes):

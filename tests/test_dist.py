@@ -235,3 +235,17 @@ def test_bench_world_mismatch():
     """A rank whose WORLD_SIZE disagrees with --gpus refuses to report."""
     rc, line, err = _bench(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert rc == 2 and line is None and "WORLD_SIZE=1" in err
+
+
+def test_bench_force_pg_one_rank():
+    """`--gpus 1 --force-pg` starts one rank under torch.distributed.run and
+    joins a process group at world size 1, so the control plane's
+    collectives run through the backend (gloo here, RCCL on the GPU box:
+    tests/test_gpu_bench.py) instead of being skipped."""
+    rc, line, err = _bench(["--gpus", "1", "--force-pg", "--streams", "6", "--eblocks", "250",
+                            "--steps", "1", "--warmup", "0", "--bad-stream", "4"])
+    assert rc == 0, err[-3000:]
+    assert line["n_gpus"] == 1 and line["backend"] == "gloo"
+    cp = line["control_plane"]
+    assert cp["shards"] == [[0, 6]] and cp["first_error_stream"] == 4
+    assert cp["checksums_match_oracle"] is True and line["bit_exact"] is True

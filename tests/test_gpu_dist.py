@@ -54,7 +54,10 @@ def _worker(rank, world, port, q, eb, bits, ch, mix, warmup, frames, init, bad):
     ("A", 8, None), ("W", 0, None),
     # a bad right block mid-range; one in rank 1's warm-up (rank 0 owns it);
     # one at rank 1's first eblock
-    ("A", 8, (100_000, 1)), ("W", 8, (150_000 - 3, 0)), ("A", 8, (150_000, 1))])
+    ("A", 8, (100_000, 1)), ("W", 8, (150_000 - 3, 0)), ("A", 8, (150_000, 1)),
+    # a bad right block in the last, cut eblock: the carried left state
+    # comes from frames 30/31 the cut PCM does not hold (round-2 ADVICE)
+    ("A", 8, (300_000, 1))])
 def test_split_two_ranks_on_gpu(built, mix, warmup, bad):
     import oracle
     world, eb, bits, ch = 2, 300_001, 8, 2
