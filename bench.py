@@ -29,7 +29,8 @@ other_configs.
 Reported:
   value       decoded MSamples/s of the whole job over the timed steps
               (barrier + synchronize on both sides, max over ranks); with
-              --pipeline D (default 2) consecutive steps run on D HIP
+              --pipeline D (default 0: 1 or 2 by a calibration run after
+              the warm-up) consecutive steps run on D HIP
               streams with their own input copy and output/workspace
               buffers (no slot can hit another's input in a cache), so one
               step's tail overlaps the next step's head; every step is a
@@ -240,6 +241,33 @@ def timed_serial(step, steps, dev):
     return time.perf_counter() - t0
 
 
+PIPE_CAL_STEPS = 10     # steps per calibration run of --pipeline 0
+
+
+def choose_depth(step, nslots, dev, want):
+    """Steps in flight for the timed region.  want >= 1: that many (up to
+    the slots made).  want == 0 (auto, the default): after the warm-up,
+    PIPE_CAL_STEPS steps one at a time and the same with every slot in
+    flight, twice each, interleaved; the faster schedule is the one timed
+    (round 2: two in flight won 4 % on C3 and lost 3-10 % on C4/C5g on the
+    driver's box).  Returns (depth, calibration ms per step or None)."""
+    if want >= 1 or nslots == 1:
+        return max(1, min(want, nslots)), None
+    import torch
+    t = {1: [], nslots: []}
+    for _ in range(2):
+        for d in (1, nslots):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for i in range(PIPE_CAL_STEPS):
+                step(i if d > 1 else 0)
+            torch.cuda.synchronize(dev)
+            t[d].append(time.perf_counter() - t0)
+    best = min(t, key=lambda d: min(t[d]))
+    return best, {"depth%d_ms" % d: round(min(v) / PIPE_CAL_STEPS * 1e3, 4)
+                  for d, v in t.items()}
+
+
 def pipeline_slots(depth, dev, make):
     """`depth` independent sets of output/workspace buffers, each with a HIP
     stream of its own (slot 0 on torch's current stream).  Consecutive steps
@@ -274,7 +302,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     xa_np = synth.stream(eb, bits, ch, args.mix, seed=rank)
     src = torch.from_numpy(xa_np).to(dev)
     ws_len = bjxa_amd.decode_workspace_size(eb, ch, args.chunk, args.warm_blocks)
-    slots = pipeline_slots(args.pipeline, dev, lambda k: {
+    slots = pipeline_slots(args.pipeline or 2, dev, lambda k: {
         "src": src if k == 0 else src.clone(),
         "dst": torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev),
         "ws": torch.zeros(ws_len, dtype=torch.uint8, device=dev),
@@ -291,19 +319,20 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
 
     for i in range(args.warmup):
         step(i)
+    depth, cal = choose_depth(step, len(slots), dev, args.pipeline)
     torch.cuda.synchronize(dev)
     if dist_on():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i if depth > 1 else 0)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if dist_on():
         dist.barrier()
 
-    serial = timed_serial(step, args.steps, dev) if len(slots) > 1 else elapsed
+    serial = timed_serial(step, args.steps, dev) if depth > 1 else elapsed
 
     # kernel timing: slot 0 alone, one launch at a time (no overlap)
     evs = EventPairs(max(EV_SAMPLES, args.steps))
@@ -345,7 +374,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
 
     xa_bytes = eb * ch * (bits * 4 + 1)
     return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
-            "elapsed": elapsed, "serial": serial, "pipeline": len(slots),
+            "elapsed": elapsed, "serial": serial, "pipeline": depth, "pipeline_cal": cal,
             "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
             "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
@@ -479,8 +508,8 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
         return {"dsts": dsts, "srcs": own,
                 "status": torch.zeros(max(n, 1) * bjxa_amd.STATUS_WORDS, dtype=torch.int32,
                                       device=dev)}
-    slots = pipeline_slots(pipeline, dev, make_slot)
-    elapsed, spec, serial = 0.0, [0.0], 0.0
+    slots = pipeline_slots(pipeline or 2, dev, make_slot)
+    elapsed, spec, serial, depth, cal = 0.0, [0.0], 0.0, 1, None
     if n:
         with contextlib.ExitStack() as stack:
             for sl in slots:
@@ -495,18 +524,19 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
                 sl["batch"].decode(sl["status"].data_ptr(), sl["sh"], ev)
             for i in range(warmup):
                 step(i)
+            depth, cal = choose_depth(step, len(slots), dev, pipeline)
             torch.cuda.synchronize(dev)
             if dist_on():
                 dist.barrier()
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             for i in range(steps):
-                step(i)
+                step(i if depth > 1 else 0)
             torch.cuda.synchronize(dev)
             elapsed = time.perf_counter() - t0
             if dist_on():
                 dist.barrier()
-            serial = timed_serial(step, steps, dev) if len(slots) > 1 else elapsed
+            serial = timed_serial(step, steps, dev) if depth > 1 else elapsed
             # kernel timing: slot 0 alone, one launch at a time
             evs = EventPairs(max(EV_SAMPLES, steps))
             for ev in evs.ev:
@@ -548,7 +578,8 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             "value": round(samples * steps / elapsed / 1e6, 1) if elapsed else 0.0,
             "unit": "MSamples/s",
             "ms_per_step": round(elapsed / steps * 1e3, 4),
-            "pipeline": len(slots), "ms_per_step_serial": round(serial / steps * 1e3, 4),
+            "pipeline": depth, "pipeline_cal": cal,
+            "ms_per_step_serial": round(serial / steps * 1e3, 4),
             "spec_ms": round(spec_ms, 4), "spec_samples": len(spec),
             "frac": round(alg / (spec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if spec_ms else 0.0,
             "alg_bytes": alg, "repaired": int(st[:, 3].sum()) if n else 0,
@@ -659,9 +690,11 @@ def parse_args(argv=None):
     ap.add_argument("--eblocks", type=int, default=0, help="C5 eblocks per stream (65,536)")
     ap.add_argument("--bad-stream", type=int, default=-1,
                     help="C5: give this stream a gain-5 profile (first-error collective)")
-    ap.add_argument("--pipeline", type=int, default=2,
+    ap.add_argument("--pipeline", type=int, default=0,
                     help="steps in flight: consecutive steps on this many HIP streams, "
-                         "each with its own output and workspace buffers")
+                         "each with its own input copy, output and workspace buffers; "
+                         "0 (default) = 1 or 2, whichever a short calibration after the "
+                         "warm-up finds faster on this workload and box")
     ap.add_argument("--force-pg", action="store_true",
                     help="join an RCCL process group even at --gpus 1 (the rank starts "
                          "under torch.distributed.run), so the control-plane collectives "
@@ -724,7 +757,8 @@ def other_stream_line(o, steps, world=1):
     return {"workload": o["desc"] + (" per rank" if world > 1 else ""),
             "value": round(job_value(o["samples"], world, steps, o["elapsed"]), 1),
             "unit": "MSamples/s", "ms_per_step": round(o["elapsed"] / steps * 1e3, 4),
-            "pipeline": o["pipeline"], "ms_per_step_serial": round(o["serial"] / steps * 1e3, 4),
+            "pipeline": o["pipeline"], "pipeline_cal": o["pipeline_cal"],
+            "ms_per_step_serial": round(o["serial"] / steps * 1e3, 4),
             "spec_ms": round(o["spec_ms"], 4), "spec_samples": o["spec_samples"],
             "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "chunk": int(o["status"][6]), "bit_exact": o["ok"], "cpu_baseline": o["cpu"]}
@@ -783,7 +817,7 @@ def main_stream(args, workload, dev, world, rank):
                    "profile_mix": args.mix, "parallelism": "independent streams, 1 per GPU",
                    "chunk": int(st[6]), "warmup_eblocks": int(st[7]),
                    "tuning": "auto" if not args.chunk and args.warm_blocks < 0 else "manual",
-                   "pipeline": r["pipeline"]},
+                   "pipeline": r["pipeline"], "pipeline_cal": r["pipeline_cal"]},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -905,7 +939,8 @@ def main_c5(args, dev, world, rank, cdev=None):
                    "workload_id": "C5", "streams": job["streams"],
                    "streams_per_rank": [hi - lo for lo, hi in job["shards"]],
                    "parallelism": "stream shards, one batched launch per GPU, RCCL control "
-                                  "plane only", "pipeline": r["pipeline"]},
+                                  "plane only", "pipeline": r["pipeline"],
+                   "pipeline_cal": r["pipeline_cal"]},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec_batch (rank 0)",
                      "achieved": round(r["alg_bytes"] / (spec_ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["frac"],

@@ -98,7 +98,12 @@ def test_bench_default_line_c3(built):
     rf = line["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["achieved"] > 0
     assert "device" not in line
-    assert line["config"]["pipeline"] == 2 and line["ms_per_step_serial"] > 0
+    # --pipeline 0 (default): the calibration picks one or two in flight
+    cfg = line["config"]
+    assert cfg["pipeline"] in (1, 2) and line["ms_per_step_serial"] > 0
+    cal = cfg["pipeline_cal"]
+    assert set(cal) == {"depth1_ms", "depth2_ms"}
+    assert cfg["pipeline"] == min((1, 2), key=lambda d: cal["depth%d_ms" % d])
 
 
 def test_bench_pipeline_slots_agree(built):

@@ -10,13 +10,14 @@ usage: python tools/pmc_summary.py gpurun_out/prof_<tag> [--json out.json]
   traffic        HBM bytes per xa_decode_spec launch:
                    write = WRITE_SIZE x 1 KiB (MI355X_MICROARCH.md §HBM: exact
                            for 16-B/lane streaming stores, which these are)
-                   read  = TCC_EA0_RDREQ x bytes-per-request, the latter
-                           calibrated on this kernel's own load pattern by the
-                           warm-up-0 pass (pmc_w0/), which loads exactly the
-                           XA stream once: bytes_per_rdreq = XA bytes /
-                           RDREQ(w0).  FETCH_SIZE raw (x1 KiB) and the
-                           guide's x2 rule for 16-B/lane reads are reported
-                           beside it for comparison.
+                   read  = TCC_EA0_RDREQ x 128 B: one request is one 128-B
+                           line, measured on known byte counts with the
+                           decode's own load forms (tools/rdreq_calib.hip,
+                           profiles/r03_rdreq_calib.json; TCC_BUBBLE reads 0,
+                           so FETCH_SIZE counts each as 64 B -- the guide's
+                           x2).  The warm-up-0 pass (pmc_w0/) gives the
+                           pattern's own overfetch (read / XA bytes with no
+                           warm-up re-read).
 """
 import csv
 import glob
@@ -24,6 +25,9 @@ import json
 import os
 import sys
 from collections import defaultdict
+
+
+RDREQ_BYTES = 128      # profiles/r03_rdreq_calib.json
 
 
 def rows(pattern):
@@ -93,12 +97,14 @@ def main():
     sp = out["pmc"].get(key, {})
     if bench and "TCC_EA0_RDREQ_sum" in sp and "TCC_EA0_RDREQ_sum" in w0.get(key, {}):
         xa_bytes = cfg["eblocks_per_rank"] * cfg["channels"] * (cfg["bits"] * 4 + 1)
-        bpr = xa_bytes / w0[key]["TCC_EA0_RDREQ_sum"]
+        bpr = RDREQ_BYTES
         read = sp["TCC_EA0_RDREQ_sum"] * bpr
         write = sp.get("WRITE_SIZE", 0.0) * 1024
         t = {"read_bytes": round(read), "write_bytes": round(write),
              "hbm_bytes_per_launch": round(read + write),
-             "bytes_per_rdreq": round(bpr, 2),
+             "bytes_per_rdreq": bpr,
+             "read_over_xa": round(read / xa_bytes, 4),
+             "read_over_xa_w0": round(w0[key]["TCC_EA0_RDREQ_sum"] * bpr / xa_bytes, 4),
              "alg_bytes_per_launch": xa_bytes + cfg["eblocks_per_rank"] * 64 * cfg["channels"]}
         if "FETCH_SIZE" in sp:
             t["fetch_size_raw_bytes"] = round(sp["FETCH_SIZE"] * 1024)

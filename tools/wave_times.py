@@ -6,6 +6,7 @@ the kernel is start-up, steady streaming and tail.
 
 usage: make -C bjxa_amd/csrc OUT=$PWD/dbg/times OBJ=$PWD/dbg/times/build EXTRA=-DXA_DBG_TIMES
        BJXA_LIB_PATH=dbg/times/libbjxa.so.0 python tools/wave_times.py [C3|C2] [mix]
+           [variant] [tag]
 """
 import json
 import os
@@ -23,11 +24,13 @@ from bjxa_amd import synth  # noqa: E402
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "C3"
     mix = sys.argv[2] if len(sys.argv) > 2 else "A"
+    variant = int(sys.argv[3], 0) if len(sys.argv) > 3 else 0
+    tag = sys.argv[4] if len(sys.argv) > 4 else ""
     eb, ch = (5_000_000, 2) if wl == "C3" else (10_000_000, 1)
     xa = synth.stream(eb, 8, ch, mix, seed=0)
     src = torch.from_numpy(xa).cuda()
     dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
-    ws_len = bjxa_amd.decode_workspace_size(eb, ch)
+    ws_len = bjxa_amd.decode_workspace_size(eb, ch, variant=variant)
     ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
     st = torch.zeros(8, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
@@ -35,7 +38,8 @@ def main():
     out = []
     for it in range(6):
         bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, 8, ch,
-                               ws.data_ptr(), ws_len, st.data_ptr(), stream=sh)
+                               ws.data_ptr(), ws_len, st.data_ptr(), stream=sh,
+                               variant=variant)
         torch.cuda.synchronize()
         s = st.cpu().numpy().view(np.uint32)
         nch = int(s[5])
@@ -48,7 +52,7 @@ def main():
         xcc = rec[:, 3] >> 16
         if it < 2:
             continue
-        np.save(os.path.join(ROOT, "gpurun_out", "wt_%s_%s_%d.npy" % (wl, mix, it)), rec)
+        np.save(os.path.join(ROOT, "gpurun_out", "wt_%s_%s%s_%d.npy" % (wl, mix, tag, it)), rec)
         r = {"waves": nw, "kernel_us": float(end.max()),
              "start_pct": [float(np.percentile(start, p)) for p in (0, 50, 90, 100)],
              "warm_end_pct": [float(np.percentile(warm, p)) for p in (0, 50, 90, 100)],
