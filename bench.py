@@ -181,6 +181,18 @@ def job_value(samples_per_rank, world, steps, elapsed):
     return samples_per_rank * world * steps / elapsed / 1e6
 
 
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cpu.max quota /
+    period), or None: a GPU box shows all its cores in the affinity mask
+    but may grant only a per-GPU share of their time."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpu():
     try:
         with open("/proc/cpuinfo") as f:
@@ -438,17 +450,20 @@ def batch_inputs(name, nstreams, eblocks, lo, hi, bad_stream=-1, mix="A"):
     return out
 
 
-def oracle_batch(inputs, threads):
+def oracle_batch(inputs, threads, outs=None):
     """Oracle decode of a list of streams on `threads` host threads (one
     decoder per thread, streams round-robin); returns {index: pcm} and the
-    seconds it took."""
+    seconds it took.  `outs` ({index: int16 array}) are output buffers
+    allocated and touched beforehand (pre-fault all buffers --
+    fresh ones page-fault inside the timed region, and hundreds of threads
+    faulting at once serialise in the kernel)."""
     import oracle
     res = {}
 
     def work(k):
         for j in range(k, len(inputs), threads):
             i, bits, ch, eb, xa = inputs[j]
-            res[i] = oracle.decode(xa, eb, bits, ch)
+            res[i] = oracle.decode(xa, eb, bits, ch, out=None if outs is None else outs[i])
     t = time.perf_counter()
     ths = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
     for th in ths:
@@ -462,16 +477,19 @@ def cpu_batch_baseline(name, inputs):
     """C4/C5 CPU baseline: the oracle on all usable host cores."""
     threads, aff, online = cpu_threads()
     samples = sum(eb * 32 * ch for _, _, ch, eb, _ in inputs)
-    oracle_batch(inputs, threads)                       # discarded first pass
-    times = [oracle_batch(inputs, threads)[1] for _ in range(CPU_PASSES)]
+    outs = {i: np.ones(eb * 32 * ch, np.int16) for i, _, ch, eb, _ in inputs}
+    oracle_batch(inputs, threads, outs)                 # discarded first pass
+    times = [oracle_batch(inputs, threads, outs)[1] for _ in range(CPU_PASSES)]
+    del outs
     med = float(np.median(times))
     return {"value": round(samples / med / 1e6, 1), "unit": "MSamples/s", "cores": threads,
-            "cores_affinity": aff, "cpus_online": online, "kind": "port",
+            "cores_affinity": aff, "cpus_online": online, "cpu_quota_cpus": cpu_quota(),
+            "kind": "port",
             "sample": "all %d streams of %s (%d samples), oracle/xa_oracle.c single-pass decode "
                       "(libbjxa's block loop restated, src/libbjxa.c:602-661), one decoder per "
                       "thread on %d threads (%d cores in the affinity mask%s), streams "
-                      "round-robin, median of %d passes after a discarded first; host: %s, "
-                      "%s CPUs online"
+                      "round-robin, output buffers pre-faulted, median of %d passes after a "
+                      "discarded first; host: %s, %s CPUs online"
                       % (len(inputs), name, samples, threads, aff,
                          "; BJXA_CPU_THREADS" if threads < aff else "", CPU_PASSES,
                          host_cpu(), online)}
@@ -611,13 +629,15 @@ def run_encode(steps, warmup, dev, verify, cpu_leg=False):
     dt = (time.perf_counter() - t0) / steps
     # per-launch kernel time: events around each of EV_SAMPLES launches
     # (encode is one kernel, so torch's events on the same stream suffice),
-    # each launch after a 512 MiB fill that evicts the 256 MiB Infinity
+    # each launch after a 512 MiB read that evicts the 256 MiB Infinity
     # Cache, so no launch reads its 640 MB input partly from the cache
-    # (round-2 VERDICT: an isolated launch otherwise times below the trace)
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    # (round-2 VERDICT: an isolated launch otherwise times below the trace).
+    # A read, not a fill: dirty fill lines would be written back during the
+    # launch and charge it for traffic that is not its own.
+    flush = torch.ones(128 << 20, dtype=torch.int32, device=dev)
     ms = []
     for i in range(max(EV_SAMPLES, steps)):
-        flush.fill_(i & 255)
+        flush.sum()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         bjxa_amd.encode_device(src.data_ptr(), frames, bits, ch, dst.data_ptr(), sh)
@@ -653,7 +673,7 @@ def run_encode(steps, warmup, dev, verify, cpu_leg=False):
             "ms_per_step": round(dt * 1e3, 4), "kernel_ms": round(med, 4),
             "kernel_samples": len(ms),
             "kernel_ms_stat": "median of %d launches, each after a 512 MiB cache-evicting "
-                              "fill" % len(ms),
+                              "read" % len(ms),
             "frac": round(alg / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "step_frac": round(alg / dt / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": alg,
             "byte_exact": ok, "cpu_baseline": cpu}

@@ -287,6 +287,8 @@ def encode_wav(data, bits=6):
 # ---- device-resident extension (include/bjxa_hip.h) ----------------------
 
 VARIANT_BALANCED = 0x20   # two-length chunk plan (include/bjxa_hip.h)
+VARIANT_STRIDED = 0x40    # the lane-strided K1
+VARIANT_REGION = 0x80     # the region kernel K1r (experimental)
 
 
 def decode_workspace_size(eblocks, channels, chunk=0, warmup=-1, variant=0):

@@ -46,11 +46,13 @@ typedef struct {
 					 * around the speculative-decode kernel */
 	uint32_t	variant;	/* bits 0-3: kernel structure, 0 = automatic
 					 * (DESIGN.md §3); bit 5: two-length chunk
-					 * plan; bits 8-11: pacing of the
-					 * speculative kernel's waves (0 = automatic,
-					 * 15 = off, n = a barrier every n groups).
-					 * Pass the same tuning to
-					 * bjxa_hip_decode_workspace. */
+					 * plan; bit 6: the lane-strided K1 even
+					 * where another is automatic; bit 7: the
+					 * region kernel (experimental); bits 8-11:
+					 * pacing of the speculative kernel's waves
+					 * (0 = automatic, 15 = off, n = a barrier
+					 * every n groups).  Pass the same tuning
+					 * to bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 
 /*

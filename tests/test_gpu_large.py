@@ -62,3 +62,4 @@ def test_auto_plan_ragged(built, bits, ch):
     c = -(-(-(-eb // 131072)) // q) * q
     assert st[6] == c and st[5] == -(-eb // c)
     assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
+
