@@ -253,21 +253,25 @@ def timed_serial(step, steps, dev):
     return time.perf_counter() - t0
 
 
-PIPE_CAL_STEPS = 10     # steps per calibration run of --pipeline 0
+PIPE_CAL_STEPS = 20     # steps per calibration run of --pipeline 0
+PIPE_CAL_ROUNDS = 3     # interleaved runs per depth
+PIPE_CAL_MARGIN = 0.01  # two in flight must win by this much
 
 
 def choose_depth(step, nslots, dev, want):
     """Steps in flight for the timed region.  want >= 1: that many (up to
     the slots made).  want == 0 (auto, the default): after the warm-up,
     PIPE_CAL_STEPS steps one at a time and the same with every slot in
-    flight, twice each, interleaved; the faster schedule is the one timed
+    flight, PIPE_CAL_ROUNDS times each, interleaved; steps in flight are
+    timed only if their median beats one at a time by PIPE_CAL_MARGIN
     (round 2: two in flight won 4 % on C3 and lost 3-10 % on C4/C5g on the
-    driver's box).  Returns (depth, calibration ms per step or None)."""
+    driver's box; on C3 the two are often within noise).  Returns (depth,
+    median calibration ms per step, or None)."""
     if want >= 1 or nslots == 1:
         return max(1, min(want, nslots)), None
     import torch
     t = {1: [], nslots: []}
-    for _ in range(2):
+    for _ in range(PIPE_CAL_ROUNDS):
         for d in (1, nslots):
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
@@ -275,9 +279,10 @@ def choose_depth(step, nslots, dev, want):
                 step(i if d > 1 else 0)
             torch.cuda.synchronize(dev)
             t[d].append(time.perf_counter() - t0)
-    best = min(t, key=lambda d: min(t[d]))
-    return best, {"depth%d_ms" % d: round(min(v) / PIPE_CAL_STEPS * 1e3, 4)
-                  for d, v in t.items()}
+    med = {d: float(np.median(v)) for d, v in t.items()}
+    best = nslots if med[nslots] < med[1] * (1.0 - PIPE_CAL_MARGIN) else 1
+    return best, {"depth%d_ms" % d: round(v / PIPE_CAL_STEPS * 1e3, 4)
+                  for d, v in med.items()}
 
 
 def pipeline_slots(depth, dev, make):

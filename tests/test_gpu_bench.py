@@ -103,7 +103,10 @@ def test_bench_default_line_c3(built):
     assert cfg["pipeline"] in (1, 2) and line["ms_per_step_serial"] > 0
     cal = cfg["pipeline_cal"]
     assert set(cal) == {"depth1_ms", "depth2_ms"}
-    assert cfg["pipeline"] == min((1, 2), key=lambda d: cal["depth%d_ms" % d])
+    # two in flight only when they beat one at a time by the margin
+    two = cal["depth2_ms"] < cal["depth1_ms"] * (1 - 0.01) - 1e-4
+    one = cal["depth2_ms"] > cal["depth1_ms"] * (1 - 0.01) + 1e-4
+    assert (cfg["pipeline"] == 2) if two else (cfg["pipeline"] == 1) if one else True
 
 
 def test_bench_pipeline_slots_agree(built):

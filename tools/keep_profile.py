@@ -36,10 +36,15 @@ def main():
               "hbm_bytes_per_launch": t["hbm_bytes_per_launch"],
               "read_bytes": t["read_bytes"], "write_bytes": t["write_bytes"],
               "bytes_per_rdreq": t["bytes_per_rdreq"],
+              "alg_bytes_per_launch": t["alg_bytes_per_launch"],
+              "traffic_over_alg": t["traffic_over_alg"],
+              "read_over_xa": t.get("read_over_xa"), "read_over_xa_w0": t.get("read_over_xa_w0"),
               "spec_kernel_us_trace": summ["kernel_us"].get(summ["spec_key"]),
               "spec_kernel_us_trace_alone": summ.get("kernel_us_alone", {}).get(summ["spec_key"]),
-              "method": "write = WRITE_SIZE x 1 KiB; read = TCC_EA0_RDREQ x bytes per "
-                        "request calibrated by a warm-up-0 pass (tools/pmc_summary.py)",
+              "method": "write = WRITE_SIZE x 1 KiB; read = TCC_EA0_RDREQ x 128 B (one "
+                        "request is one 128-B line: tools/rdreq_calib.hip, "
+                        "profiles/r03_rdreq_calib.json); per spec launch, L2->fabric "
+                        "requests, Infinity-Cache hits included (tools/pmc_summary.py)",
               "source": "profiles/%s_summary.json" % name}
     with open(os.path.join(dst, "pmc_latest.json"), "w") as f:
         json.dump(latest, f, indent=1, sort_keys=True)
