@@ -52,7 +52,8 @@ def main():
                          "larger allocations (a multiple of 16)")
     ap.add_argument("--eblocks", type=int, default=0,
                     help="single-stream workloads: override the stream length")
-    ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps"],
+    ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps", "gaps2m",
+                                                        "skew"],
                     help="batches: one allocation per stream buffer (sep) or all "
                          "streams back to back in one allocation (packed)")
     ap.add_argument("builds", nargs="+")
@@ -74,16 +75,23 @@ def main():
         else:
             inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)),
                                         mix=args.mix)
-        if args.layout in ("packed", "gaps"):
+        if args.layout in ("packed", "gaps", "gaps2m", "skew"):
             # every stream in one allocation, back to back at 256-B steps
-            # (gaps: plus a seeded random gap of 0-255 x 256 B before each)
+            # (gaps: plus a seeded random gap of 0-255 x 256 B before each;
+            # gaps2m: 0-31 x 64 KiB; skew: stream i at +(37 i mod 32) x
+            # 64 KiB + (i mod 16) x 4 KiB)
             rng = np.random.default_rng(7)
 
             def carve(sizes):
                 offs, o = [], 0
-                for n in sizes:
+                for k, n in enumerate(sizes):
                     if args.layout == "gaps":
                         o += int(rng.integers(0, 256)) * 256
+                    elif args.layout == "gaps2m":
+                        o += int(rng.integers(0, 32)) * 65536
+                    elif args.layout == "skew":
+                        o = (o + (1 << 21) - 1) // (1 << 21) * (1 << 21) + \
+                            ((37 * k) % 32) * 65536 + (k % 16) * 4096
                     offs.append(o)
                     o += (n + 255) // 256 * 256
                 big = torch.empty(o, dtype=torch.uint8, device="cuda")
