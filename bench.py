@@ -494,10 +494,12 @@ def cpu_batch_baseline(name, inputs):
                       "(libbjxa's block loop restated, src/libbjxa.c:602-661), one decoder per "
                       "thread on %d threads (%d cores in the affinity mask%s), streams "
                       "round-robin, output buffers pre-faulted, median of %d passes after a "
-                      "discarded first; host: %s, %s CPUs online"
+                      "discarded first; host: %s, %s CPUs online%s"
                       % (len(inputs), name, samples, threads, aff,
                          "; BJXA_CPU_THREADS" if threads < aff else "", CPU_PASSES,
-                         host_cpu(), online)}
+                         host_cpu(), online,
+                         "" if cpu_quota() is None else
+                         ", cgroup quota %.1f CPUs of time" % cpu_quota())}
 
 
 def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, eblocks=0,
