@@ -289,6 +289,8 @@ def encode_wav(data, bits=6):
 VARIANT_BALANCED = 0x20   # two-length chunk plan (include/bjxa_hip.h)
 VARIANT_STRIDED = 0x40    # the lane-strided K1
 VARIANT_REGION = 0x80     # the region kernel K1r (experimental)
+VARIANT_SPLIT = 0x1000    # batches: split PCM lane strides on the 4 KiB grid
+VARIANT_SPLITW = 0x2000   # the split with the full warm-up on the long chunks
 
 
 def decode_workspace_size(eblocks, channels, chunk=0, warmup=-1, variant=0):
@@ -320,13 +322,14 @@ class Batch:
     `streams` is a list of dicts with d_src, d_dst, eblocks, bits, channels
     and optional frames (default eblocks*32) and state."""
 
-    def __init__(self, streams, chunk=0, warmup=-1, stream=0):
+    def __init__(self, streams, chunk=0, warmup=-1, stream=0, variant=0):
         arr = (HipStream * len(streams))()
         for i, d in enumerate(streams):
             arr[i] = HipStream(d["d_src"], d["d_dst"], d.get("frames", d["eblocks"] * 32),
                                d["eblocks"], d["bits"], d["channels"],
                                (ctypes.c_int16 * 4)(*d.get("state", (0, 0, 0, 0))))
         t = HipTuning(chunk, warmup)
+        t.variant = variant
         self.n = len(streams)
         self._p = lib().bjxa_hip_batch_new(arr, self.n, ctypes.byref(t), stream)
         if not self._p:

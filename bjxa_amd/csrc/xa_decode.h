@@ -39,9 +39,14 @@ struct xa_dec_args {
 	uint32_t eblocks;
 	uint32_t nchunks;
 	uint32_t C, W;		/* chunk and warm-up lengths in eblocks */
-	uint32_t nlong;		/* chunks [0, nlong) are C + Q long (Q =
-				 * XA_CHUNK_Q(ch), nlong % 64 == 0); chunk q
-				 * starts at eblock q*C + Q*min(q, nlong) */
+	uint32_t nlong;		/* chunks [0, nlong) are C + dlong long
+				 * (nlong % 256 == 0 or past the last
+				 * chunk); chunk q starts at eblock
+				 * q*C + dlong*min(q, nlong) */
+	uint32_t dlong;		/* a multiple of XA_CHUNK_Q(ch) */
+	uint32_t Wlong;		/* warm-up of the long chunks (W: the
+				 * others); Wlong + dlong == W gives every
+				 * lane the same super-step count */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
 	uint32_t pace;		/* K1 waves of a workgroup wait for each other
 				 * every `pace` groups (0 = never) */
@@ -88,7 +93,8 @@ struct xa_batch_stream {		/* 64 B, device table entry */
 	uint32_t C;			/* chunk length, eblocks */
 	uint32_t init[2];
 	uint32_t fmt;			/* bits | channels << 8 */
-	uint32_t pad[3];
+	uint32_t nlong, dlong, Wlong;	/* two chunk lengths, as in
+					 * xa_dec_args (nlong 0: one) */
 };
 
 /* per-stream control words (xa_batch_args::sctl) */

@@ -259,10 +259,11 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 	uint8_t *land = region, *ost = region + g2::HALF;
 	const uint32_t chunk = wchunk0 + lane;
 	const int64_t eblocks = a.eblocks;
-	const uint32_t Cw = a.C + (wchunk0 < a.nlong ? (uint32_t)g::G2 : 0u);
-	const int64_t wstart = chunk_start<g::G2>(a, wchunk0);
+	const bool lng = wchunk0 < a.nlong;
+	const uint32_t Cw = a.C + (lng ? a.dlong : 0u);
+	const int64_t wstart = chunk_start(a, wchunk0);
 	const int64_t b0 = wstart + (int64_t)lane * Cw;
-	const int W = (int)a.W;
+	const int W = (int)(lng ? a.Wlong : a.W);
 	/* super-steps: NW of warm-up, then NC of the chunk (W and Cw are
 	 * multiples of 2G, the host plans them so) */
 	const int NW = W / (2 * G), NS = NW + (int)Cw / (2 * G);
@@ -546,8 +547,8 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 	if (CH == 2)
 		xa_unpack_state(s.y, p0[CH - 1], p1[CH - 1]);
 	const int64_t eblocks = a.eblocks;
-	const int64_t b0 = chunk_start<g::G2>(a, q);
-	int64_t b1 = chunk_start<g::G2>(a, q + 1);
+	const int64_t b0 = chunk_start(a, q);
+	int64_t b1 = chunk_start(a, q + 1);
 	if (b1 > eblocks)
 		b1 = eblocks;
 	const int64_t ndw = (eblocks * EBSZ + 3) / 4;
@@ -994,8 +995,12 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.eblocks = d.eblocks;
 	a.nchunks = d.nchunks;
 	a.C = d.C;
-	a.W = b.W;
-	a.nlong = 0;
+	/* two chunk lengths: the short chunks' warm-up makes their lanes'
+	 * super-step count that of the long ones */
+	a.W = d.nlong ? d.Wlong + d.dlong : b.W;
+	a.nlong = d.nlong;
+	a.dlong = d.dlong;
+	a.Wlong = d.nlong ? d.Wlong : b.W;
 	a.pace = 0;	/* the batch kernel decides per workgroup */
 	a.rep_C = a.rep_chunks = 0;
 	a.init[0] = d.init[0];
@@ -1034,13 +1039,17 @@ xa_decode_spec_batch(xa_batch_args b)
 	const uint32_t w0 = blockIdx.x * XA_SPEC_WPB;
 	bool lockstep = b.pace != 0u && w0 + XA_SPEC_WPB <= b.nwaves;
 	if (lockstep) {
-		const uint32_t s0 = b.wstream[w0];
-		const uint32_t c0 = b.streams[s0].C, f0 = b.streams[s0].fmt >> 8;
-		for (int k = 1; k < XA_SPEC_WPB; k++) {
-			const uint32_t sk = b.wstream[w0 + k];
-			lockstep = lockstep && b.streams[sk].C == c0 &&
-			    (b.streams[sk].fmt >> 8) == f0;
-		}
+		/* a wave's lane length (warm-up + chunk: the same for both
+		 * chunk lengths of a stream) and channel count */
+		auto shape = [&](uint32_t wk) {
+			const xa_batch_stream &d = b.streams[b.wstream[wk]];
+			const uint32_t len = d.nlong == 0u ? b.W + d.C :
+			    d.Wlong + d.dlong + d.C;
+			return len | (d.fmt >> 8) << 24;
+		};
+		const uint32_t s0 = shape(w0);
+		for (int k = 1; k < XA_SPEC_WPB; k++)
+			lockstep = lockstep && shape(w0 + k) == s0;
 	}
 	lockstep = __builtin_amdgcn_readfirstlane(lockstep);
 	if (w >= b.nwaves)
@@ -1203,7 +1212,8 @@ xa_decode_fix_batch(xa_batch_args b)
 	 * then the last chunk's exit state) overlap across streams */
 	constexpr int XA_PUB = 4;
 	for (uint32_t s0 = 0; s0 < b.nstreams; s0 += 256u * XA_PUB) {
-		uint32_t err[XA_PUB], fix[XA_PUB], tail[XA_PUB], nch[XA_PUB], cc[XA_PUB];
+		uint32_t err[XA_PUB], fix[XA_PUB], tail[XA_PUB], nch[XA_PUB], cc[XA_PUB],
+		    ww[XA_PUB];
 		uint2 fin[XA_PUB];
 #pragma unroll
 		for (int k = 0; k < XA_PUB; k++) {
@@ -1212,6 +1222,7 @@ xa_decode_fix_batch(xa_batch_args b)
 			const uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
 			nch[k] = d.nchunks;
 			cc[k] = d.C;
+			ww[k] = d.nlong ? d.Wlong + d.dlong : b.W;
 			fin[k] = b.e[d.cbase + d.nchunks - 1];
 			err[k] = sc[XA_SCTL_ERR];
 			fix[k] = sc[XA_SCTL_FIXED];
@@ -1231,7 +1242,7 @@ xa_decode_fix_batch(xa_batch_args b)
 			st[XA_ST_TAIL] = tail[k];
 			st[XA_ST_CHUNKS] = nch[k];
 			st[XA_ST_C] = cc[k];
-			st[XA_ST_W] = b.W;
+			st[XA_ST_W] = ww[k];
 			sc[XA_SCTL_ERR] = 0xffffffffu;
 			sc[XA_SCTL_FIXED] = 0;
 			sc[XA_SCTL_TAIL] = 0;

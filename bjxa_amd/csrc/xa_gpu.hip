@@ -33,6 +33,8 @@
 #define XA_VARIANT_BALANCED	0x20u	/* two-length chunk plan */
 #define XA_VARIANT_STRIDED	0x40u	/* the lane-strided K1 instead of K1r */
 #define XA_VARIANT_REGION	0x80u	/* K1r (experimental, opt-in) */
+#define XA_VARIANT_SPLIT	0x1000u	/* batches: split 4-KiB lane strides (opt-in) */
+#define XA_VARIANT_SPLITW	0x2000u	/* the split with the full warm-up on long chunks */
 
 /* a HIP device is visible; probed once per process, thread-safe */
 extern "C" int
@@ -267,6 +269,8 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.C = p.C;
 	a.W = p.W;
 	a.nlong = p.nlong;
+	a.dlong = XA_CHUNK_Q(s->channels);
+	a.Wlong = p.W;
 	a.pace = pick_pace((p.W + p.C) / XA_CHUNK_Q(s->channels), false, tune);
 	a.init[0] = ((uint32_t)(uint16_t)s->state[0]) |
 	    ((uint32_t)(uint16_t)s->state[1] << 16);
@@ -369,6 +373,54 @@ stream_ok(const bjxa_hip_stream_t *s)
 }
 
 /*
+ * Split stride.  A stream whose PCM lane stride (c * 64 * ch bytes) is a
+ * multiple of 4 KiB -- C5's streams of 65,536 eblocks give 8 KiB at the
+ * per-GPU share of 8 GPUs, 16-64 KiB at 4-1 GPUs -- starts every lane's
+ * PCM lines at the same address modulo the HBM interleave, and K1 then
+ * runs 25-40 % slower.  Such a stream of an even number k
+ * of waves gets two chunk lengths instead: its first k/2 waves c + Q, the
+ * others c - Q (Q = the chunk quantum), both strides off the 4 KiB grid,
+ * covering the same 64kc eblocks.  The long chunks warm up over W - Q
+ * eblocks and the short ones over W + Q, so every lane still runs W + c
+ * (no idle lanes, no longer kernel); XA_VARIANT_SPLITW keeps W for the long
+ * chunks (W + 2Q for the short).  Opt-in (XA_VARIANT_SPLIT or _SPLITW):
+ * it takes C5g's 128 streams packed in one allocation from 0.432 to
+ * 0.358 ms, but costs 2 % (spec) and 5 % (step, more repairs at W - Q) in
+ * separate allocations and 2.5 % on C5.
+ */
+static void
+split_stride(xa_batch_stream &h, uint32_t E, uint32_t ch, uint32_t c,
+    uint32_t k, uint32_t W, const bjxa_hip_tuning_t *tune, uint32_t *nch)
+{
+	const uint32_t Q = XA_CHUNK_Q(ch);
+	const uint32_t v = tune ? tune->variant : 0u;
+	h.nlong = h.dlong = h.Wlong = 0;
+	if (!(v & (XA_VARIANT_SPLIT | XA_VARIANT_SPLITW)) || (c * ch) % 64u != 0 ||
+	    k < 2 || k % 2 ||
+	    c < MIN_CHUNK + Q)
+		return;
+	/* W - Q must leave the long chunks a warm-up (not so for mono at
+	 * W = 8, nor at W < 2Q) */
+	if (!(v & XA_VARIANT_SPLITW) && W < 2u * Q)
+		return;
+	const uint32_t wl = (v & XA_VARIANT_SPLITW) ? W : W - Q;
+	const uint32_t C = c - Q, nl = 32u * k, dl = 2u * Q;
+	const uint64_t cover = (uint64_t)nl * (C + dl);
+	uint64_t n;
+	if (cover >= E)
+		n = (E + C + dl - 1) / (C + dl);
+	else
+		n = nl + (E - cover + C - 1) / C;
+	if (n > 64ull * k)
+		return;
+	h.C = C;
+	h.nlong = nl;
+	h.dlong = dl;
+	h.Wlong = wl;
+	*nch = (uint32_t)n;
+}
+
+/*
  * Plan: one budget of channel blocks per lane, Cb = the batch's channel
  * blocks / target_lanes() (at least MIN_CHUNK, a multiple of 4); a stream of
  * E eblocks and ch channels gets k = round(E*ch / (64*Cb)) >= 1 whole
@@ -419,6 +471,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	cb = (cb + 3) & ~(uint64_t)3;
 	const uint32_t w = (tune && tune->warmup >= 0) ? (uint32_t)tune->warmup :
 	    DEFAULT_WARMUP;
+	const uint32_t W = (w + 7) & ~7u;	/* a whole chunk quantum of every format */
 
 	xa_batch_stream *hs = (xa_batch_stream *)calloc(n, sizeof *hs);
 	if (hs == NULL) {
@@ -436,14 +489,16 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		if (c < MIN_CHUNK)
 			c = MIN_CHUNK;
 		c = (c + G - 1) / G * G;
-		const uint32_t nch = (uint32_t)((E + c - 1) / c);
+		uint32_t nch = (uint32_t)((E + c - 1) / c);
+		split_stride(hs[i], E, ch, (uint32_t)c, (uint32_t)k, W, tune, &nch);
 		hs[i].src = (const uint8_t *)s[i].d_src;
 		hs[i].dst = (uint8_t *)s[i].d_dst;
 		hs[i].pcm_bytes = s[i].frames * 2u * ch;
 		hs[i].eblocks = E;
 		hs[i].nchunks = nch;
 		hs[i].cbase = (uint32_t)(64 * nwaves);
-		hs[i].C = (uint32_t)c;
+		if (hs[i].nlong == 0)
+			hs[i].C = (uint32_t)c;
 		hs[i].init[0] = ((uint32_t)(uint16_t)s[i].state[0]) |
 		    ((uint32_t)(uint16_t)s[i].state[1] << 16);
 		hs[i].init[1] = ((uint32_t)(uint16_t)s[i].state[2]) |
@@ -517,7 +572,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	a.wstream = (const uint32_t *)(ws + o_wav);
 	a.nstreams = n;
 	a.nwaves = (uint32_t)nwaves;
-	a.W = (w + 7) & ~7u;	/* a whole chunk quantum of every format */
+	a.W = W;
 	/* super-steps of a lane: its channel blocks (warm-up included) over
 	 * the 8 per super-step, the same for every format */
 	a.pace = pick_pace((uint32_t)((a.W * 2u + cb) / 8u), true, tune);

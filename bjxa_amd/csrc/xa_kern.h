@@ -55,12 +55,11 @@ template <int BITS, int CH> struct geo {
 	static constexpr int OB = 64 * CH;		/* PCM bytes per eblock */
 };
 
-/* first eblock of chunk q (chunks [0, nlong) are G longer; G = G2) */
-template <int G>
+/* first eblock of chunk q (chunks [0, nlong) are dlong longer) */
 __device__ __forceinline__ int64_t
 chunk_start(const xa_dec_args &a, uint32_t q)
 {
-	return (int64_t)q * a.C + (int64_t)G * min(q, a.nlong);
+	return (int64_t)q * a.C + (int64_t)a.dlong * min(q, a.nlong);
 }
 
 /*

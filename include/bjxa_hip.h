@@ -51,8 +51,13 @@ typedef struct {
 					 * region kernel (experimental); bits 8-11:
 					 * pacing of the speculative kernel's waves
 					 * (0 = automatic, 15 = off, n = a barrier
-					 * every n groups).  Pass the same tuning
-					 * to bjxa_hip_decode_workspace. */
+					 * every n groups); batches: bit 12: split
+					 * PCM lane strides on the 4 KiB grid into
+					 * two chunk lengths, bit 13: the same
+					 * with the full warm-up on the long
+					 * chunks (both experimental).  Pass
+					 * the same tuning to
+					 * bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 
 /*
