@@ -60,6 +60,11 @@ def main():
              "per_xcd_end_max": [float(end[xcc == x].max()) for x in range(8)],
              "per_xcd_end_med": [float(np.median(end[xcc == x])) for x in range(8)],
              "per_xcd_waves": [int((xcc == x).sum()) for x in range(8)],
+             "per_xcd_dur_med": [float(np.median((end - start)[xcc == x])) for x in range(8)],
+             # dispatch: the XCD that workgroup b lands on, by b % 8
+             "xcd_of_block_mod8": [int(np.bincount(xcc[(np.arange(nw) // 4) % 8 == m],
+                                                   minlength=8).argmax()) for m in range(8)],
+             "block_mod8_match": float(np.mean(xcc == ((np.arange(nw) // 4) % 8))),
              "dur_pct": [float(np.percentile(end - start, p)) for p in (0, 50, 100)]}
         out.append(r)
         print(json.dumps(r), flush=True)
