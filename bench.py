@@ -10,8 +10,11 @@ bjxa_hip_decode_async (speculative decode + verify/repair/tail).  The same
 run measures, under "other_configs": C2 (one 8-bit mono stream of 10M
 blocks), C4 (1024 mixed-format streams per launch), C5 (the whole 1024-stream
 job on this GPU: the N = 1 point of the scaling curve), C5g (one GPU's share
-of C5 at 8 GPUs) and the encode direction on C3-shaped PCM.  --no-other
-skips them.
+of C5 at 8 GPUs) and the encode direction on C3-shaped PCM, each in a child
+process of its own started before this one touches the GPU, so every
+configuration allocates its buffers in a fresh process as a caller (or one
+rank of the N > 1 job) would (in one process the C5g
+share landed where it ran 20 % slower).  --no-other skips them.
 
 N > 1 (`--gpus N`): BASELINE config C5 -- 1024 8-bit stereo streams of
 65,536 eblocks, a fixed job split into contiguous shares, one rank per GPU,
@@ -730,7 +733,52 @@ def parse_args(argv=None):
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true",
                     help="skip the other_configs lines")
+    ap.add_argument("--only-other", default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+def other_child(name, args):
+    """other_configs[name], measured by a child bench.py (--only-other) in a
+    process of its own; the parent has not touched the GPU yet."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--only-other", name,
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--mix", args.mix,
+           "--pipeline", str(args.pipeline)]
+    cmd += ["--no-cpu"] if args.no_cpu else []
+    cmd += ["--no-verify"] if args.no_verify else []
+    p = subprocess.run(cmd, stdout=subprocess.PIPE)
+    if p.returncode != 0:
+        raise RuntimeError("bench.py --only-other %s: exit status %d" % (name, p.returncode))
+    return json.loads(p.stdout.decode().strip().splitlines()[-1])
+
+
+def other_configs(args, workload):
+    """Every other_configs line at N = 1 beside `workload`'s, each from its
+    own child process."""
+    names = [n for n in sorted(WORKLOADS) if n != workload] + sorted(BATCHES) + ["encode_C3"]
+    return {n: other_child(n, args) for n in names}
+
+
+def only_other(args):
+    """Child side of other_child: one other_configs line on GPU 0."""
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    name, cpu_leg, verify = args.only_other, not args.no_cpu, not args.no_verify
+    if name in WORKLOADS:
+        o = other_stream_line(run_workload(name, args, dev, 1, 0, verify, cpu_leg), args.steps)
+    elif name in BATCHES:
+        o = run_batch(name, args.steps, args.warmup, dev, verify, cpu_leg=cpu_leg,
+                      pipeline=args.pipeline)
+        for k in ("checksums", "ref_checksums", "shard"):
+            o.pop(k)
+        if o["first_error"] == FIRST_ERR_NONE:
+            o["first_error"] = None
+    elif name == "encode_C3":
+        o = run_encode(args.steps, args.warmup, dev, verify, cpu_leg)
+    else:
+        raise ValueError(name)
+    print(json.dumps(o), flush=True)
+    return 0
 
 
 def main():
@@ -742,6 +790,8 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.only_other:
+        return only_other(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -766,15 +816,20 @@ def main():
         finally:
             if world > 1:
                 dist.destroy_process_group()
+    workload = args.workload or ("C3" if world == 1 else "C5")
+    # the other configurations first, in child processes, while this one
+    # has not touched the GPU
+    others = other_configs(args, workload) if (world == 1 and not args.force_pg and
+                                               workload in WORKLOADS and
+                                               not args.no_other) else None
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or args.force_pg:
         dist.init_process_group("nccl", device_id=dev)
-    workload = args.workload or ("C3" if world == 1 else "C5")
     try:
         if workload == "C5":
             return main_c5(args, dev, world, rank)
-        return main_stream(args, workload, dev, world, rank)
+        return main_stream(args, workload, dev, world, rank, others)
     finally:
         if dist_on():
             dist.destroy_process_group()
@@ -791,34 +846,19 @@ def other_stream_line(o, steps, world=1):
             "chunk": int(o["status"][6]), "bit_exact": o["ok"], "cpu_baseline": o["cpu"]}
 
 
-def main_stream(args, workload, dev, world, rank):
-    """C3 (or C2): one stream per rank, weak scaling."""
+def main_stream(args, workload, dev, world, rank, others=None):
+    """C3 (or C2): one stream per rank, weak scaling; `others`: the
+    other_configs lines (other_configs(), measured before this)."""
     cpu_leg = rank == 0 and world == 1 and not args.no_cpu
     r = run_workload(workload, args, dev, world, rank, not args.no_verify, cpu_leg)
     elapsed, ok = r["elapsed"], r["ok"]
     if dist_on():
         elapsed, ok = reduce_over_ranks(elapsed, ok, dev)
 
-    other = {}
-    if world == 1 and not args.no_other:
-        for name in sorted(WORKLOADS):
-            if name == workload:
-                continue
-            o = run_workload(name, args, dev, 1, rank, not args.no_verify, cpu_leg)
-            other[name] = other_stream_line(o, args.steps)
-            ok = ok if o["ok"] in (None, True) else False
-        for name in sorted(BATCHES):
-            o = run_batch(name, args.steps, args.warmup, dev, not args.no_verify,
-                          cpu_leg=cpu_leg, pipeline=args.pipeline)
-            for k in ("checksums", "ref_checksums", "shard"):
-                o.pop(k)
-            if o["first_error"] == FIRST_ERR_NONE:
-                o["first_error"] = None
-            other[name] = o
-            ok = ok if o["bit_exact"] in (None, True) else False
-        o = run_encode(args.steps, args.warmup, dev, not args.no_verify, cpu_leg)
-        other["encode_C3"] = o
-        ok = ok if o["byte_exact"] in (None, True) else False
+    other = others or {}
+    for o in other.values():
+        exact = o.get("bit_exact", o.get("byte_exact"))
+        ok = ok if exact in (None, True) else False
 
     st = r["status"]
     achieved = r["alg_bytes"] / (r["spec_ms"] * 1e-3) / 1e9

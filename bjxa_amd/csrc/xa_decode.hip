@@ -756,6 +756,12 @@ drain_tail(const xa_dec_args &a)
 #ifndef XA_FIX_CPT
 #define XA_FIX_CPT 2
 #endif
+#ifndef XA_FIXB_MAXWG
+#define XA_FIXB_MAXWG 256u	/* batch K2 workgroups at most */
+#endif
+#ifndef XA_FIXB_WPB
+#define XA_FIXB_WPB 4u		/* batch K2 waves per workgroup */
+#endif
 #ifndef XA_FIX_REL
 #define XA_FIX_REL 0
 #endif
@@ -1149,7 +1155,7 @@ fix_uniform(const xa_dec_args &a, uint32_t fmt, uint32_t q, uint2 s, uint2 &ex)
  * workgroup (arrival ticket) drains the cascades and publishes every
  * stream's status.
  */
-__global__ __launch_bounds__(256) void
+__global__ __launch_bounds__(64 * XA_FIXB_WPB) void
 xa_decode_fix_batch(xa_batch_args b)
 {
 	__shared__ uint32_t last;
@@ -1158,7 +1164,8 @@ xa_decode_fix_batch(xa_batch_args b)
 	const uint64_t *e64 = (const uint64_t *)b.e;
 	const uint64_t *g64 = (const uint64_t *)b.g;
 	bool wrote = false;
-	for (uint32_t gw = blockIdx.x * 4u + wv; gw < b.nwaves; gw += gridDim.x * 4u) {
+	for (uint32_t gw = blockIdx.x * XA_FIXB_WPB + wv; gw < b.nwaves;
+	    gw += gridDim.x * XA_FIXB_WPB) {
 		const uint32_t sid = __builtin_amdgcn_readfirstlane(b.wstream[gw]);
 		const xa_dec_args a = batch_stream_args(b, sid);
 		const uint32_t cbase = __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
@@ -1211,13 +1218,14 @@ xa_decode_fix_batch(xa_batch_args b)
 	 * in full before any is written, so the dependent loads (descriptor,
 	 * then the last chunk's exit state) overlap across streams */
 	constexpr int XA_PUB = 4;
-	for (uint32_t s0 = 0; s0 < b.nstreams; s0 += 256u * XA_PUB) {
+	for (uint32_t s0 = 0; s0 < b.nstreams; s0 += 64u * XA_FIXB_WPB * XA_PUB) {
 		uint32_t err[XA_PUB], fix[XA_PUB], tail[XA_PUB], nch[XA_PUB], cc[XA_PUB],
 		    ww[XA_PUB];
 		uint2 fin[XA_PUB];
 #pragma unroll
 		for (int k = 0; k < XA_PUB; k++) {
-			const uint32_t sid = min(s0 + threadIdx.x + 256u * k, b.nstreams - 1);
+			const uint32_t sid = min(s0 + threadIdx.x + 64u * XA_FIXB_WPB * k,
+			    b.nstreams - 1);
 			const xa_batch_stream &d = b.streams[sid];
 			const uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
 			nch[k] = d.nchunks;
@@ -1230,7 +1238,7 @@ xa_decode_fix_batch(xa_batch_args b)
 		}
 #pragma unroll
 		for (int k = 0; k < XA_PUB; k++) {
-			const uint32_t sid = s0 + threadIdx.x + 256u * k;
+			const uint32_t sid = s0 + threadIdx.x + 64u * XA_FIXB_WPB * k;
 			if (sid >= b.nstreams)
 				continue;
 			uint32_t *sc = b.sctl + sid * XA_SCTL_WORDS;
@@ -1259,16 +1267,18 @@ xa_decode_batch_launch(const xa_batch_args &b, hipStream_t st, hipEvent_t ev0,
     hipEvent_t ev1)
 {
 	const unsigned grid = (b.nwaves + XA_SPEC_WPB - 1) / XA_SPEC_WPB;
-	/* K2: a wave per global wave, 4 per workgroup, at most 256 workgroups */
-	unsigned grid2 = (b.nwaves + 3u) / 4u;
-	if (grid2 > 256u)
-		grid2 = 256u;
+	/* K2: a wave per global wave, XA_FIXB_WPB per workgroup, at most
+	 * XA_FIXB_MAXWG workgroups */
+	unsigned grid2 = (b.nwaves + XA_FIXB_WPB - 1) / XA_FIXB_WPB;
+	if (grid2 > XA_FIXB_MAXWG)
+		grid2 = XA_FIXB_MAXWG;
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
 	hipLaunchKernelGGL((xa_decode_spec_batch<128, true>), dim3(grid),
 	    dim3(64 * XA_SPEC_WPB), 0, st, b);
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
-	hipLaunchKernelGGL(xa_decode_fix_batch, dim3(grid2), dim3(256), 0, st, b);
+	hipLaunchKernelGGL(xa_decode_fix_batch, dim3(grid2), dim3(64 * XA_FIXB_WPB), 0,
+	    st, b);
 	return hipGetLastError();
 }

@@ -143,3 +143,17 @@ def test_bench_c5_rccl_one_rank(built):
     assert cp["checksums_match_oracle"] is True and line["bit_exact"] is True
     assert cp["shards"] == [[0, 24]]
     assert "device" not in line
+
+
+@pytest.mark.parametrize("name", ["C5g", "encode_C3"])
+def test_bench_other_config_child(built, name):
+    """The child side of other_configs (bench.py --only-other): one line,
+    measured in its own process, bit-exact against the oracle."""
+    rc, line, err = _bench(["--only-other", name, "--steps", "3", "--warmup", "1",
+                            "--no-cpu"])
+    assert rc == 0, err[-2000:]
+    if name == "C5g":
+        assert line["bit_exact"] is True and line["streams"] == 128
+        assert line["first_error"] is None and 0 < line["spec_ms"] < line["ms_per_step"] * 2
+    else:
+        assert line["byte_exact"] is True
