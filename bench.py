@@ -135,6 +135,7 @@ class EventPairs:
 
     def __init__(self, n):
         self.hip = hip_runtime()
+        self.hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         self.ev = []
         for _ in range(n):
             a, b = ctypes.c_void_p(), ctypes.c_void_p()
@@ -256,6 +257,45 @@ def timed_serial(step, steps, dev):
     return time.perf_counter() - t0
 
 
+def timed_region(step, steps, depth, slots, dev):
+    """The timed region: `steps` steps (consecutive slots when depth > 1,
+    else slot 0), bracketed by a barrier (N > 1) and device synchronizes.
+    Each step is also bracketed by hipEvents recorded on its slot's stream,
+    so the line can show the spread of the steps inside the window.
+    Returns (wall seconds, per-step event ms)."""
+    import torch
+    import torch.distributed as dist
+    evs = EventPairs(steps)
+    rec = evs.hip.hipEventRecord
+    torch.cuda.synchronize(dev)
+    if dist_on():
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        k = i if depth > 1 else 0
+        sh = slots[k % len(slots)]["sh"]
+        rec(evs.ev[i][0], sh)
+        step(k)
+        rec(evs.ev[i][1], sh)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist_on():
+        dist.barrier()
+    ms = evs.ms()
+    evs.close()
+    return elapsed, ms
+
+
+def spread(ms):
+    """min / median / max of per-step event times (ms)"""
+    if not ms:
+        return None
+    return {"min": round(float(np.min(ms)), 4), "median": round(float(np.median(ms)), 4),
+            "max": round(float(np.max(ms)), 4), "n": len(ms),
+            "what": "hipEvents around each step of the timed region, on its stream"}
+
+
 PIPE_CAL_STEPS = 20     # steps per calibration run of --pipeline 0
 PIPE_CAL_ROUNDS = 3     # interleaved runs per depth
 PIPE_CAL_MARGIN = 0.01  # two in flight must win by this much
@@ -340,17 +380,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     for i in range(args.warmup):
         step(i)
     depth, cal = choose_depth(step, len(slots), dev, args.pipeline)
-    torch.cuda.synchronize(dev)
-    if dist_on():
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i if depth > 1 else 0)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist_on():
-        dist.barrier()
+    elapsed, step_ms = timed_region(step, args.steps, depth, slots, dev)
 
     serial = timed_serial(step, args.steps, dev) if depth > 1 else elapsed
 
@@ -395,7 +425,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     xa_bytes = eb * ch * (bits * 4 + 1)
     return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
             "elapsed": elapsed, "serial": serial, "pipeline": depth, "pipeline_cal": cal,
-            "spec_ms": float(np.median(spec_ms)),
+            "step_ms": spread(step_ms), "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
             "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
 
@@ -537,7 +567,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
                 "status": torch.zeros(max(n, 1) * bjxa_amd.STATUS_WORDS, dtype=torch.int32,
                                       device=dev)}
     slots = pipeline_slots(pipeline or 2, dev, make_slot)
-    elapsed, spec, serial, depth, cal = 0.0, [0.0], 0.0, 1, None
+    elapsed, spec, serial, depth, cal, step_ms = 0.0, [0.0], 0.0, 1, None, []
     if n:
         with contextlib.ExitStack() as stack:
             for sl in slots:
@@ -553,17 +583,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             for i in range(warmup):
                 step(i)
             depth, cal = choose_depth(step, len(slots), dev, pipeline)
-            torch.cuda.synchronize(dev)
-            if dist_on():
-                dist.barrier()
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            for i in range(steps):
-                step(i if depth > 1 else 0)
-            torch.cuda.synchronize(dev)
-            elapsed = time.perf_counter() - t0
-            if dist_on():
-                dist.barrier()
+            elapsed, step_ms = timed_region(step, steps, depth, slots, dev)
             serial = timed_serial(step, steps, dev) if depth > 1 else elapsed
             # kernel timing: slot 0 alone, one launch at a time
             evs = EventPairs(max(EV_SAMPLES, steps))
@@ -605,7 +625,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             "samples": samples, "elapsed": elapsed,
             "value": round(samples * steps / elapsed / 1e6, 1) if elapsed else 0.0,
             "unit": "MSamples/s",
-            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "step_ms": spread(step_ms),
             "pipeline": depth, "pipeline_cal": cal,
             "ms_per_step_serial": round(serial / steps * 1e3, 4),
             "spec_ms": round(spec_ms, 4), "spec_samples": len(spec),
@@ -841,6 +861,7 @@ def other_stream_line(o, steps, world=1):
             "unit": "MSamples/s", "ms_per_step": round(o["elapsed"] / steps * 1e3, 4),
             "pipeline": o["pipeline"], "pipeline_cal": o["pipeline_cal"],
             "ms_per_step_serial": round(o["serial"] / steps * 1e3, 4),
+            "step_ms": o["step_ms"],
             "spec_ms": round(o["spec_ms"], 4), "spec_samples": o["spec_samples"],
             "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "chunk": int(o["status"][6]), "bit_exact": o["ok"], "cpu_baseline": o["cpu"]}
@@ -873,6 +894,7 @@ def main_stream(args, workload, dev, world, rank, others=None):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "ms_per_step_serial": round(r["serial"] / args.steps * 1e3, 4),
+        "step_ms": r["step_ms"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -997,7 +1019,8 @@ def main_c5(args, dev, world, rank, cdev=None):
         "value": round(job["samples"] * args.steps / elapsed / 1e6, 1), "unit": "MSamples/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "ms_per_step_serial": r["ms_per_step_serial"], "higher_is_better": True,
+        "ms_per_step_serial": r["ms_per_step_serial"], "step_ms": r["step_ms"],
+        "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int32+f32",
         "data": "synthetic (seeded XA streams, profile mix A, uniform codes)",
         "config": {"workload": BATCHES["C5"] if not (args.streams or args.eblocks) else
@@ -1007,7 +1030,11 @@ def main_c5(args, dev, world, rank, cdev=None):
                    "streams_per_rank": [hi - lo for lo, hi in job["shards"]],
                    "parallelism": "stream shards, one batched launch per GPU, RCCL control "
                                   "plane only", "pipeline": r["pipeline"],
-                   "pipeline_cal": r["pipeline_cal"]},
+                   "pipeline_cal": r["pipeline_cal"],
+                   "scaling_n1_ref": "other_configs.C5 of the N = 1 line (python bench.py): "
+                                     "this same job on one GPU, the first point of the "
+                                     "strong-scaling curve (the N = 1 headline itself is "
+                                     "C3, one stream)"},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec_batch (rank 0)",
                      "achieved": round(r["alg_bytes"] / (spec_ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["frac"],

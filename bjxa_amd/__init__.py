@@ -286,11 +286,7 @@ def encode_wav(data, bits=6):
 
 # ---- device-resident extension (include/bjxa_hip.h) ----------------------
 
-VARIANT_BALANCED = 0x20   # two-length chunk plan (include/bjxa_hip.h)
-VARIANT_STRIDED = 0x40    # the lane-strided K1
-VARIANT_REGION = 0x80     # the region kernel K1r (experimental)
-VARIANT_SPLIT = 0x1000    # batches: split PCM lane strides on the 4 KiB grid
-VARIANT_SPLITW = 0x2000   # the split with the full warm-up on the long chunks
+VARIANT_PACE_OFF = 15 << 8   # tuning variant bits 8-11: no pacing barriers
 
 
 def decode_workspace_size(eblocks, channels, chunk=0, warmup=-1, variant=0):

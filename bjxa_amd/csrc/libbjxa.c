@@ -118,7 +118,9 @@ read_all(void *buf, size_t n, FILE *file)
 #define OFFLOAD_ENCODE_DEFAULT	4096u
 
 static uint64_t offload_min[2];
-static int fault_gpu_decode;	/* BJXA_TEST_FAULT=gpu-decode (tests only) */
+#ifdef BJXA_TEST_HOOKS
+static int fault_gpu_decode;	/* BJXA_TEST_FAULT=gpu-decode */
+#endif
 static pthread_once_t offload_once = PTHREAD_ONCE_INIT;
 
 /* a threshold: decimal digits only, no sign, no blanks, no overflow */
@@ -158,12 +160,15 @@ offload_init(void)
 		}
 		__atomic_store_n(&offload_min[d], n, __ATOMIC_RELAXED);
 	}
-	/* fault injection for the CLI tests: a call routed to the device
-	 * fails with EIO before anything is decoded, with or without a GPU */
+#ifdef BJXA_TEST_HOOKS
+	/* fault injection for the CLI tests (test build only, make
+	 * testhooks): a call routed to the device fails with EIO before
+	 * anything is decoded, with or without a GPU */
 	{
 		const char *f = getenv("BJXA_TEST_FAULT");
 		fault_gpu_decode = f != NULL && strcmp(f, "gpu-decode") == 0;
 	}
+#endif
 	errno = saved;
 }
 
@@ -175,6 +180,7 @@ on_gpu(int dir, uint64_t eblocks)
 	    bjxa__gpu_present();
 }
 
+#ifdef BJXA_TEST_HOOKS
 /* BJXA_TEST_FAULT=gpu-decode and a call the threshold sends to the device */
 static int
 gpu_decode_faulted(uint64_t eblocks)
@@ -183,6 +189,7 @@ gpu_decode_faulted(uint64_t eblocks)
 	return fault_gpu_decode && eblocks >= __atomic_load_n(
 	    &offload_min[BJXA_HIP_OFFLOAD_DECODE], __ATOMIC_RELAXED);
 }
+#endif
 
 int64_t
 bjxa_hip_offload_threshold(int direction, int64_t eblocks)
@@ -411,8 +418,10 @@ bjxa_decode(bjxa_decoder_t *dec, void *dst, size_t dst_len, const void *src,
 		copy = f->data_len_pcm;
 
 	memcpy(st, dec->state, sizeof st);
+#ifdef BJXA_TEST_HOOKS
 	if (gpu_decode_faulted(n))
 		FAIL(EIO);
+#endif
 	if (!on_gpu(BJXA_HIP_OFFLOAD_DECODE, n)) {
 		(void)bjxa__cpu_decode(src, (uint32_t)n, dec->bits,
 		    dec->channels, st, dst, copy, &err_cb);

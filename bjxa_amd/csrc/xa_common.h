@@ -51,14 +51,6 @@ xa_step(int32_t top, uint32_t sh, int32_t k0, int32_t k1, int32_t &p0,
     int32_t &p1)
 {
 	int32_t t = top >> sh;
-#if defined(XA_DBG_STEP)
-	/* diagnostic build only (wrong output): no predictor */
-	(void)k0;
-	(void)k1;
-	p1 = p0;
-	p0 = t;
-	return t;
-#endif
 	int32_t g = __mul24(p0, k0) + __mul24(p1, k1);
 	int32_t s = t + ((g + (int32_t)((uint32_t)(g >> 31) >> 24)) >> 8);
 	s = min(max(s, -32768), 32767);
@@ -93,12 +85,6 @@ typedef float xa_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t
 xa_step_lr(uint32_t t, xa_f2 k0, xa_f2 k1, xa_f2 &p0, xa_f2 &p1)
 {
-#if defined(XA_DBG_STEP)
-	(void)k0;
-	(void)k1;
-	p1 = p0;
-	return t;
-#endif
 	const xa_f2 g = __builtin_elementwise_fma(p0, k0, p1 * k1);
 	const int32_t sl = (int32_t)g.x + (int32_t)(int16_t)(t & 0xffffu);
 	const int32_t sr = (int32_t)g.y + (int32_t)(int16_t)(t >> 16);
@@ -125,12 +111,6 @@ template <bool HI>
 __device__ __forceinline__ int32_t
 xa_step_f(uint32_t t, float k0, float k1, float &p0, float &p1)
 {
-#if defined(XA_DBG_STEP)
-	(void)k0;
-	(void)k1;
-	p1 = p0;
-	return (int32_t)(int16_t)(HI ? t >> 16 : t & 0xffffu);
-#endif
 	const float g = __builtin_fmaf(p0, k0, p1 * k1);
 	int32_t s = (int32_t)g + (int32_t)(int16_t)(HI ? t >> 16 : t & 0xffffu);
 	s = min(max(s, -32768), 32767);

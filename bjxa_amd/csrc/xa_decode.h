@@ -12,6 +12,7 @@
 #define XA_CTL_NQ	1	/* re-check queue length */
 #define XA_CTL_FIXED	2	/* chunks repaired by K2 */
 #define XA_CTL_TICKET	3	/* K2 workgroups finished (last one runs the tail) */
+#define XA_CTL_NL	4	/* chunks K1 listed for K2 (inner-wave mismatches) */
 #define XA_CTL_WORDS	64	/* 256 B */
 
 /* status words written by the tail kernel */
@@ -38,44 +39,29 @@ struct xa_dec_args {
 	uint64_t pcm_bytes;	/* PCM bytes to emit (last block may be cut) */
 	uint32_t eblocks;
 	uint32_t nchunks;
-	uint32_t C, W;		/* chunk and warm-up lengths in eblocks */
-	uint32_t nlong;		/* chunks [0, nlong) are C + dlong long
-				 * (nlong % 256 == 0 or past the last
-				 * chunk); chunk q starts at eblock
-				 * q*C + dlong*min(q, nlong) */
-	uint32_t dlong;		/* a multiple of XA_CHUNK_Q(ch) */
-	uint32_t Wlong;		/* warm-up of the long chunks (W: the
-				 * others); Wlong + dlong == W gives every
-				 * lane the same super-step count */
+	uint32_t C, W;		/* chunk and warm-up lengths in eblocks
+				 * (multiples of XA_CHUNK_Q(ch)); chunk q
+				 * starts at eblock q*C */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
 	uint32_t pace;		/* K1 waves of a workgroup wait for each other
 				 * every `pace` groups (0 = never) */
 	uint2 *g, *e;		/* per-chunk entry / exit state */
-	uint32_t *queue;	/* re-check queue, nchunks entries */
+	uint32_t *queue;	/* re-check queue, 2 * nchunks entries */
+	uint32_t *list;		/* K1 -> K2: chunks whose entry differs from
+				 * the exit of the chunk before them in the
+				 * same wave, nchunks entries (batches: the
+				 * batch's list, global chunk indices) */
+	uint32_t *nlist;	/* its length (ctl[XA_CTL_NL] of the launch) */
+	uint32_t lbase;		/* list entry = lbase + chunk (batches: the
+				 * stream's first global chunk) */
 	uint32_t *ctl;		/* XA_CTL_WORDS */
 	uint32_t *status;	/* XA_ST_WORDS */
-	uint32_t rep_C, rep_chunks;	/* reported as the status' chunk length
-					 * and count when nonzero (the region
-					 * kernel's K2 runs over regions) */
 };
 
+/* K1 (decode, verify inside each workgroup) and K2 (boundaries between
+ * K1 workgroups, cascades, status) on `st`; ev0/ev1 (optional) around K1 */
 hipError_t xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
-    unsigned variant, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
-
-/*
- * Region kernel (K1r, xa_decode.hip): lane chunks of XA_REGION_C(ch)
- * eblocks with a warm-up of XA_REGION_W, 64 chunks per wave-region; `a.C`,
- * `a.W` and `a.nchunks` describe the lane chunks, `a.g`/`a.e` need one entry
- * per region (ceil(nchunks / 64)).  ncu: compute units of the device (the
- * persistent grid).
- */
-#define XA_REGION_C(ch)	((ch) == 2 ? 8u : 16u)
-#define XA_REGION_W	8u
-/* K2 alone (xa_decode.hip), over a.nchunks chunks of a.C eblocks */
-hipError_t xa_decode_fix_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
-    hipStream_t st);
-hipError_t xa_decode_region_launch(const xa_dec_args &a, unsigned bits,
-    unsigned ch, unsigned ncu, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+    hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 
 /*
  * Batched decode: many independent streams, mixed formats, one launch per
@@ -93,14 +79,14 @@ struct xa_batch_stream {		/* 64 B, device table entry */
 	uint32_t C;			/* chunk length, eblocks */
 	uint32_t init[2];
 	uint32_t fmt;			/* bits | channels << 8 */
-	uint32_t nlong, dlong, Wlong;	/* two chunk lengths, as in
-					 * xa_dec_args (nlong 0: one) */
+	uint32_t pad[3];
 };
 
-/* per-stream control words (xa_batch_args::sctl) */
+/* per-stream control words (xa_batch_args::sctl); ERR and FIXED sit where
+ * xa_dec_args::ctl has them, so a stream's sctl serves as its ctl */
 #define XA_SCTL_ERR	0
-#define XA_SCTL_FIXED	1
-#define XA_SCTL_TAIL	2
+#define XA_SCTL_TAIL	1
+#define XA_SCTL_FIXED	2
 #define XA_SCTL_WORDS	4
 
 struct xa_batch_args {
@@ -111,7 +97,8 @@ struct xa_batch_args {
 	uint32_t pace;			/* as xa_dec_args::pace */
 	uint2 *g, *e;			/* per global chunk */
 	uint32_t *queue;		/* 2 * 64 * nwaves */
-	uint32_t *ctl;			/* XA_CTL_WORDS (NQ, TICKET) */
+	uint32_t *list;			/* 64 * nwaves (xa_dec_args::list) */
+	uint32_t *ctl;			/* XA_CTL_WORDS (NQ, TICKET, NL) */
 	uint32_t *sctl;			/* XA_SCTL_WORDS per stream */
 	uint32_t *status;		/* XA_ST_WORDS per stream */
 };

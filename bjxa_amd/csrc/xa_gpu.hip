@@ -23,18 +23,13 @@
  * Automatic chunking: about target_lanes() chunks -- two resident 256-lane
  * workgroups on each CU of the current device (256 on MI355X), whose
  * memory pipelines bound the speculative kernel.  Uniform chunks of
- * ceil(eblocks / lanes) rounded up to the group measured best (C3: 40
- * eblocks, 489 workgroups; C2: 80); an exactly balanced plan of 512
- * workgroups with two chunk lengths (XA_VARIANT_BALANCED) was 12 % slower
- * ("Tuning").
+ * ceil(eblocks / lanes) rounded up to the chunk quantum measured best (C3:
+ * 40 eblocks, 489 workgroups; C2: 80).  Plans measured slower and removed
+ * (DESIGN.md §3 "Tuning", §5): an exactly balanced one of 512 workgroups
+ * with two chunk lengths (12 %), the region kernel K1r (1.7x, R3-2), two
+ * chunk lengths per batch stream (R3-8).
  */
 #define MAX_DEVICES	64
-#define XA_VARIANT_STRUCT	0xfu	/* kernel structure, 0 = automatic */
-#define XA_VARIANT_BALANCED	0x20u	/* two-length chunk plan */
-#define XA_VARIANT_STRIDED	0x40u	/* the lane-strided K1 instead of K1r */
-#define XA_VARIANT_REGION	0x80u	/* K1r (experimental, opt-in) */
-#define XA_VARIANT_SPLIT	0x1000u	/* batches: split 4-KiB lane strides (opt-in) */
-#define XA_VARIANT_SPLITW	0x2000u	/* the split with the full warm-up on long chunks */
 
 /* a HIP device is visible; probed once per process, thread-safe */
 extern "C" int
@@ -77,38 +72,11 @@ round_up(uint32_t v, uint32_t m)
 }
 
 struct plan {
-	uint32_t	C, W;		/* base chunk and warm-up, eblocks */
-	uint32_t	nlong;		/* leading chunks that are C + G long */
+	uint32_t	C, W;		/* chunk and warm-up, eblocks */
 	uint32_t	nchunks;
-	uint32_t	nstate;		/* entries of the g/e arrays (K2's chunks) */
-	bool		region;		/* the region kernel (K1r) */
 };
 
-/*
- * The region kernel (K1r, xa_decode.hip) is the automatic choice: fixed lane
- * chunks (XA_REGION_C) and warm-up (XA_REGION_W), K2 over regions of 64
- * chunks.  An explicit chunk or warm-up, the two-length plan, a kernel
- * structure (variant bits 0-3) or XA_VARIANT_STRIDED select the
- * lane-strided K1.
- */
-static bool
-use_region(const bjxa_hip_tuning_t *t)
-{
-	if (t == NULL || !(t->variant & XA_VARIANT_REGION))
-		return false;
-	return t->chunk == 0 && (t->warmup < 0 || (uint32_t)t->warmup == XA_REGION_W) &&
-	    (t->variant & (XA_VARIANT_STRUCT | XA_VARIANT_BALANCED |
-	    XA_VARIANT_STRIDED)) == 0;
-}
-
-/*
- * Chunk plan for one stream.  Automatic: uniform chunks (above).  With
- * XA_VARIANT_BALANCED: exactly target_lanes() chunks once the stream is long
- * enough, C = eblocks per lane rounded down to the chunk quantum (G =
- * XA_CHUNK_Q(ch) eblocks) and the remainder spread as whole quanta over the leading
- * chunks, rounded up to whole waves so every wave has one chunk length.
- * An explicit tune->chunk gives uniform chunks of that length.
- */
+/* chunk plan for one stream: automatic (above), or tune->chunk eblocks */
 static void
 plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
     struct plan *p)
@@ -117,47 +85,16 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 	const uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup :
 	    DEFAULT_WARMUP;
 	uint32_t c;
-	p->region = use_region(t);
-	if (p->region) {
-		p->C = XA_REGION_C(ch);
-		p->W = XA_REGION_W;
-		p->nlong = 0;
-		p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
-		p->nstate = (p->nchunks + 63u) / 64u;
-		return;
-	}
 	p->W = round_up(w, G);
-	p->nlong = 0;
 	if (t && t->chunk) {
 		c = t->chunk;
-	} else if (!(t && (t->variant & XA_VARIANT_BALANCED))) {
+	} else {
 		c = (uint32_t)(((uint64_t)eblocks + lanes - 1) / lanes);
 		if (c < MIN_CHUNK)
 			c = MIN_CHUNK;
-	} else {
-		c = eblocks / lanes / G * G;
-		if (c >= MIN_CHUNK) {
-			const uint64_t rest = (uint64_t)eblocks -
-			    (uint64_t)lanes * c;
-			const uint32_t nl = round_up((uint32_t)((rest + G - 1) / G),
-			    64u);
-			const uint64_t cover = (uint64_t)nl * (c + G);
-			p->C = c;
-			p->nlong = nl;
-			if (cover >= eblocks)
-				p->nchunks = (uint32_t)((eblocks + c + G - 1) /
-				    (c + G));
-			else
-				p->nchunks = nl + (uint32_t)((eblocks - cover +
-				    c - 1) / c);
-			p->nstate = p->nchunks;
-			return;
-		}
-		c = MIN_CHUNK;
 	}
 	p->C = round_up(c, G);
 	p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
-	p->nstate = p->nchunks;
 }
 
 /*
@@ -185,21 +122,11 @@ pick_pace(uint32_t ns, bool batch, const bjxa_hip_tuning_t *t)
 	return ns <= (batch ? PACE_MAX_NS_BATCH : PACE_MAX_NS) ? 1u : 0u;
 }
 
-/* kernel structure (xa_decode.hip launch()): bit 1 = non-temporal PCM
- * stores, bits 2-3 = store-phase bytes per lane (measured, DESIGN.md §5:
- * stereo NT + one eblock = 128 B; mono NT + 128 B) */
-static unsigned
-pick_variant(unsigned ch, const bjxa_hip_tuning_t *t)
-{
-	if (t && (t->variant & XA_VARIANT_STRUCT))
-		return t->variant & XA_VARIANT_STRUCT;
-	return ch == 2 ? 2u : 2u | (1u << 2);
-}
-
 static size_t
 ws_bytes(uint32_t nchunks)
 {
-	return XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 8) + 64;	/* g, e, queue (2x: the tail heap may hold duplicates) */
+	/* g, e, queue (2x: the tail heap may hold duplicates), K1's list */
+	return XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 8 + 4) + 64;
 }
 
 extern "C" size_t
@@ -210,7 +137,7 @@ bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
 	if (channels != 1 && channels != 2)
 		return 0;
 	plan_chunks(eblocks, channels, tune, &p);
-	return ws_bytes(p.nstate);
+	return ws_bytes(p.nchunks);
 }
 
 __global__ void
@@ -268,31 +195,27 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.nchunks = p.nchunks;
 	a.C = p.C;
 	a.W = p.W;
-	a.nlong = p.nlong;
-	a.dlong = XA_CHUNK_Q(s->channels);
-	a.Wlong = p.W;
 	a.pace = pick_pace((p.W + p.C) / XA_CHUNK_Q(s->channels), false, tune);
 	a.init[0] = ((uint32_t)(uint16_t)s->state[0]) |
 	    ((uint32_t)(uint16_t)s->state[1] << 16);
 	a.init[1] = ((uint32_t)(uint16_t)s->state[2]) |
 	    ((uint32_t)(uint16_t)s->state[3] << 16);
-	a.rep_C = a.rep_chunks = 0;
-	if (ws_len < ws_bytes(p.nstate)) {
+	if (ws_len < ws_bytes(p.nchunks)) {
 		errno = EINVAL;
 		return -1;
 	}
 	uint8_t *ws = (uint8_t *)d_ws;
 	a.ctl = (uint32_t *)ws;
 	a.g = (uint2 *)(ws + XA_CTL_WORDS * 4);
-	a.e = a.g + p.nstate;
-	a.queue = (uint32_t *)(a.e + p.nstate);
+	a.e = a.g + p.nchunks;
+	a.queue = (uint32_t *)(a.e + p.nchunks);
+	a.list = a.queue + 2 * (size_t)p.nchunks;
+	a.nlist = &a.ctl[XA_CTL_NL];
+	a.lbase = 0;
 	a.status = d_status;
 	hipEvent_t e0 = tune ? (hipEvent_t)tune->ev_spec[0] : NULL;
 	hipEvent_t e1 = tune ? (hipEvent_t)tune->ev_spec[1] : NULL;
-	const hipError_t rc = p.region ?
-	    xa_decode_region_launch(a, s->bits, s->channels, target_lanes() / 512u,
-	    (hipStream_t)stream, e0, e1) :
-	    xa_decode_launch(a, s->bits, s->channels, pick_variant(s->channels, tune),
+	const hipError_t rc = xa_decode_launch(a, s->bits, s->channels,
 	    (hipStream_t)stream, e0, e1);
 	if (rc != hipSuccess) {
 		errno = EIO;
@@ -355,8 +278,8 @@ xa_batch_init(uint32_t *ctl, uint32_t *sctl, uint32_t n)
 		ctl[threadIdx.x] = 0;
 	if (i < n) {
 		sctl[i * XA_SCTL_WORDS + XA_SCTL_ERR] = 0xffffffffu;
-		sctl[i * XA_SCTL_WORDS + XA_SCTL_FIXED] = 0;
 		sctl[i * XA_SCTL_WORDS + XA_SCTL_TAIL] = 0;
+		sctl[i * XA_SCTL_WORDS + XA_SCTL_FIXED] = 0;
 		sctl[i * XA_SCTL_WORDS + 3] = 0;
 	}
 }
@@ -370,54 +293,6 @@ stream_ok(const bjxa_hip_stream_t *s)
 	    s->frames <= (uint64_t)s->eblocks * 32u &&
 	    s->frames > (uint64_t)(s->eblocks - 1) * 32u &&
 	    ((uintptr_t)s->d_src & 3u) == 0 && ((uintptr_t)s->d_dst & 15u) == 0;
-}
-
-/*
- * Split stride.  A stream whose PCM lane stride (c * 64 * ch bytes) is a
- * multiple of 4 KiB -- C5's streams of 65,536 eblocks give 8 KiB at the
- * per-GPU share of 8 GPUs, 16-64 KiB at 4-1 GPUs -- starts every lane's
- * PCM lines at the same address modulo the HBM interleave, and K1 then
- * runs 25-40 % slower.  Such a stream of an even number k
- * of waves gets two chunk lengths instead: its first k/2 waves c + Q, the
- * others c - Q (Q = the chunk quantum), both strides off the 4 KiB grid,
- * covering the same 64kc eblocks.  The long chunks warm up over W - Q
- * eblocks and the short ones over W + Q, so every lane still runs W + c
- * (no idle lanes, no longer kernel); XA_VARIANT_SPLITW keeps W for the long
- * chunks (W + 2Q for the short).  Opt-in (XA_VARIANT_SPLIT or _SPLITW):
- * it takes C5g's 128 streams packed in one allocation from 0.432 to
- * 0.358 ms, but costs 2 % (spec) and 5 % (step, more repairs at W - Q) in
- * separate allocations and 2.5 % on C5.
- */
-static void
-split_stride(xa_batch_stream &h, uint32_t E, uint32_t ch, uint32_t c,
-    uint32_t k, uint32_t W, const bjxa_hip_tuning_t *tune, uint32_t *nch)
-{
-	const uint32_t Q = XA_CHUNK_Q(ch);
-	const uint32_t v = tune ? tune->variant : 0u;
-	h.nlong = h.dlong = h.Wlong = 0;
-	if (!(v & (XA_VARIANT_SPLIT | XA_VARIANT_SPLITW)) || (c * ch) % 64u != 0 ||
-	    k < 2 || k % 2 ||
-	    c < MIN_CHUNK + Q)
-		return;
-	/* W - Q must leave the long chunks a warm-up (not so for mono at
-	 * W = 8, nor at W < 2Q) */
-	if (!(v & XA_VARIANT_SPLITW) && W < 2u * Q)
-		return;
-	const uint32_t wl = (v & XA_VARIANT_SPLITW) ? W : W - Q;
-	const uint32_t C = c - Q, nl = 32u * k, dl = 2u * Q;
-	const uint64_t cover = (uint64_t)nl * (C + dl);
-	uint64_t n;
-	if (cover >= E)
-		n = (E + C + dl - 1) / (C + dl);
-	else
-		n = nl + (E - cover + C - 1) / C;
-	if (n > 64ull * k)
-		return;
-	h.C = C;
-	h.nlong = nl;
-	h.dlong = dl;
-	h.Wlong = wl;
-	*nch = (uint32_t)n;
 }
 
 /*
@@ -489,16 +364,14 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		if (c < MIN_CHUNK)
 			c = MIN_CHUNK;
 		c = (c + G - 1) / G * G;
-		uint32_t nch = (uint32_t)((E + c - 1) / c);
-		split_stride(hs[i], E, ch, (uint32_t)c, (uint32_t)k, W, tune, &nch);
+		const uint32_t nch = (uint32_t)((E + c - 1) / c);
 		hs[i].src = (const uint8_t *)s[i].d_src;
 		hs[i].dst = (uint8_t *)s[i].d_dst;
 		hs[i].pcm_bytes = s[i].frames * 2u * ch;
 		hs[i].eblocks = E;
 		hs[i].nchunks = nch;
 		hs[i].cbase = (uint32_t)(64 * nwaves);
-		if (hs[i].nlong == 0)
-			hs[i].C = (uint32_t)c;
+		hs[i].C = (uint32_t)c;
 		hs[i].init[0] = ((uint32_t)(uint16_t)s[i].state[0]) |
 		    ((uint32_t)(uint16_t)s[i].state[1] << 16);
 		hs[i].init[1] = ((uint32_t)(uint16_t)s[i].state[2]) |
@@ -531,7 +404,8 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	const size_t o_g = o_wav + al64(nwaves * 4);
 	const size_t o_e = o_g + nc * 8;
 	const size_t o_q = o_e + nc * 8;
-	const size_t len = o_q + 2 * nc * 4;
+	const size_t o_l = o_q + 2 * nc * 4;
+	const size_t len = o_l + nc * 4;
 	uint8_t *ws = NULL;
 	if (ws_cache != NULL && *ws_cap >= len) {
 		ws = (uint8_t *)*ws_cache;
@@ -579,6 +453,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	a.g = (uint2 *)(ws + o_g);
 	a.e = (uint2 *)(ws + o_e);
 	a.queue = (uint32_t *)(ws + o_q);
+	a.list = (uint32_t *)(ws + o_l);
 	a.ctl = (uint32_t *)ws;
 	a.sctl = (uint32_t *)(ws + o_sctl);
 	a.status = NULL;

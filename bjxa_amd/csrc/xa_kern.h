@@ -1,7 +1,6 @@
 /*
- * xa_kern.h -- device building blocks shared by the decode kernels
- * (xa_decode.hip: the lane-strided K1, K2, the batch kernels;
- * xa_region.hip: the region kernel K1r).  Internal.
+ * xa_kern.h -- device building blocks of the decode kernels
+ * (xa_decode.hip: K1, K2 and their batch forms).  Internal.
  */
 #ifndef BJXA_XA_KERN_H
 #define BJXA_XA_KERN_H
@@ -54,13 +53,6 @@ template <int BITS, int CH> struct geo {
 	static constexpr int GDW = BSZ;			/* dwords per group */
 	static constexpr int OB = 64 * CH;		/* PCM bytes per eblock */
 };
-
-/* first eblock of chunk q (chunks [0, nlong) are dlong longer) */
-__device__ __forceinline__ int64_t
-chunk_start(const xa_dec_args &a, uint32_t q)
-{
-	return (int64_t)q * a.C + (int64_t)a.dlong * min(q, a.nlong);
-}
 
 /*
  * Decode the channel blocks of one eblock whose first byte is byte O of w,

@@ -127,7 +127,7 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
         f = device_bytes(dst + off, 4 * ch).view(np.int16).reshape(2, ch)
         return {c: (int(f[1][c]), int(f[0][c])) for c in chans}
 
-    keep = []      # full-block scratch PCM of a cut last block, alive while used
+    keep = []      # the latest full-block scratch PCM of a cut last block
 
     def run(first, state):
         """Decode [first, hi) from `state`.  Always whole blocks (as
@@ -143,7 +143,7 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
         out = dst
         if fr < n * 32:
             full = torch.empty(n * 64 * ch, dtype=torch.uint8, device="cuda")
-            keep.append(full)
+            keep[:] = [full]      # decode() reads frame states from the latest only
             out = full.data_ptr()
         ws_len = bjxa_amd.decode_workspace_size(n, ch)
         ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
@@ -186,21 +186,30 @@ def device_range_decoder(d_src_range, d_dst_range, lo, hi, frames, bits, channel
     return decode
 
 
+_HIP = []
+
+
+def _hip():
+    """libamdhip64 through ctypes, loaded once (the runtime torch already
+    brought in)."""
+    if not _HIP:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_int]
+        _HIP.append(hip)
+    return _HIP[0]
+
+
 def device_copy(d_to, d_from, nbytes):
     """hipMemcpy device to device (synchronous)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so.7")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    if nbytes and hip.hipMemcpy(d_to, d_from, nbytes, 3) != 0:
+    if nbytes and _hip().hipMemcpy(d_to, d_from, nbytes, 3) != 0:
         raise RuntimeError("hipMemcpy failed")
 
 
 def device_bytes(d_ptr, nbytes):
     """Copy nbytes from device pointer d_ptr into a host numpy array."""
-    import ctypes
     out = np.empty(nbytes, dtype=np.uint8)
-    hip = ctypes.CDLL("libamdhip64.so.7")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    if hip.hipMemcpy(out.ctypes.data, d_ptr, nbytes, 2) != 0:
+    if _hip().hipMemcpy(out.ctypes.data, d_ptr, nbytes, 2) != 0:
         raise RuntimeError("hipMemcpy failed")
     return out

@@ -44,19 +44,11 @@ typedef struct {
 	int32_t		warmup;		/* speculative warm-up eblocks, -1 = auto */
 	void		*ev_spec[2];	/* hipEvent_t pair recorded on `stream`
 					 * around the speculative-decode kernel */
-	uint32_t	variant;	/* bits 0-3: kernel structure, 0 = automatic
-					 * (DESIGN.md §3); bit 5: two-length chunk
-					 * plan; bit 6: the lane-strided K1 even
-					 * where another is automatic; bit 7: the
-					 * region kernel (experimental); bits 8-11:
-					 * pacing of the speculative kernel's waves
-					 * (0 = automatic, 15 = off, n = a barrier
-					 * every n groups); batches: bit 12: split
-					 * PCM lane strides on the 4 KiB grid into
-					 * two chunk lengths, bit 13: the same
-					 * with the full warm-up on the long
-					 * chunks (both experimental).  Pass
-					 * the same tuning to
+	uint32_t	variant;	/* bits 8-11: pacing of the speculative
+					 * kernel's waves (0 = automatic, 15 =
+					 * off, n = a barrier every n groups);
+					 * other bits reserved (0).  Pass the
+					 * same tuning to
 					 * bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 

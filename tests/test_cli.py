@@ -19,15 +19,17 @@ import pytest
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 BJXA = os.path.join(ROOT, "bjxa_amd", "bjxa")
+# the test build (make testhooks): the same library with BJXA_TEST_FAULT
+BJXA_TH = os.path.join(ROOT, "bjxa_amd", "testhooks", "bjxa")
 FIXTURES = ["square-mono-4.xa", "square-mono-6.xa", "square-mono-8.xa",
             "square-stereo-4.xa", "square-stereo-6.xa", "square-stereo-8.xa"]
 
 
-def run(args, stdin=b"", env=None, cwd=None):
+def run(args, stdin=b"", env=None, cwd=None, exe=BJXA):
     e = dict(os.environ)
     if env:
         e.update(env)
-    p = subprocess.run([BJXA] + args, input=stdin, capture_output=True, env=e,
+    p = subprocess.run([exe] + args, input=stdin, capture_output=True, env=e,
                        cwd=cwd, timeout=120)
     return p.returncode, p.stdout, p.stderr.decode(errors="replace")
 
@@ -271,18 +273,29 @@ def test_sub_block_stream(cli):
 def test_decode_device_failure_writes_no_pcm(cli, golden, shape, route):
     """A decode call that fails for any reason other than a bad profile
     (here EIO, injected by BJXA_TEST_FAULT on every call the offload
-    threshold sends to the device) leaves nothing decoded in the buffer:
-    the CLI writes the RIFF header and no PCM, then the error (ADVICE r02:
-    never PCM of a failed call)."""
+    threshold sends to the device -- a hook only the test build has) leaves
+    nothing decoded in the buffer: the CLI writes the RIFF header and no
+    PCM, then the error (never PCM of a failed call)."""
+    assert os.access(BJXA_TH, os.X_OK), "test build missing (make -C bjxa_amd/csrc testhooks)"
     data = golden("square-stereo-8.xa")
     env = route_env(route, shape)
     env["BJXA_TEST_FAULT"] = "gpu-decode"
     if route == "cpu":
         env["BJXA_OFFLOAD_DECODE"] = "1"
-    rc, out, err = run(["decode"], data, env=env)
+    rc, out, err = run(["decode"], data, env=env, exe=BJXA_TH)
     assert rc != 0 and "bjxa_decode: Input/output error" in err
     want, _, _ = expected_decode(data)
     assert out == want[:44]
+
+
+def test_shipped_library_has_no_fault_hook(cli, golden):
+    """The shipped libbjxa.so.0 ignores BJXA_TEST_FAULT (no
+    test hook in the product path): the same call decodes normally."""
+    data = golden("square-stereo-8.xa")
+    env = dict(no_gpu(), BJXA_TEST_FAULT="gpu-decode", BJXA_OFFLOAD_DECODE="1")
+    rc, out, err = run(["decode"], data, env=env)
+    assert rc == 0, err
+    assert out == expected_decode(data)[0]
 
 
 @pytest.mark.parametrize("value", ["-1", " 5", "+5", "12x", "99999999999999999999999", ""])

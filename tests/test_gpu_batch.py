@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 FORMATS = [(8, 2), (6, 2), (4, 2), (8, 1), (6, 1), (4, 1)]
 
 
-def run_batch(specs, chunk=0, warmup=-1, repeat=1, variant=0):
+def run_batch(specs, chunk=0, warmup=-1, repeat=1):
     """specs: list of (xa bytes, eblocks, bits, ch, frames, state).  Returns
     (pcm list, status array [n, 8])."""
     torch = require_gpu()
@@ -28,7 +28,7 @@ def run_batch(specs, chunk=0, warmup=-1, repeat=1, variant=0):
                         "bits": bits, "channels": ch, "frames": frames, "state": state})
     status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    with bjxa_amd.Batch(streams, chunk, warmup, sh, variant) as b:
+    with bjxa_amd.Batch(streams, chunk, warmup, sh) as b:
         for _ in range(repeat):
             b.decode(status.data_ptr(), sh)
         torch.cuda.synchronize()
@@ -155,45 +155,26 @@ def test_batch_c4_full_size(built):
     assert not bad, bad[:10]
 
 
-@pytest.mark.parametrize("variant", [bjxa_amd.VARIANT_SPLIT, bjxa_amd.VARIANT_SPLITW])
-def test_batch_split_stride(built, variant):
-    """With VARIANT_SPLIT, streams whose PCM lane stride falls on the 4 KiB
-    grid (here 64 channel blocks per lane: stereo c = 32, 4 KiB) get two
-    chunk lengths, c + Q for their first half of waves and c - Q after, the
-    long chunks warming up over W - Q (or W with VARIANT_SPLITW).  Exact
-    fits, ragged lengths, cut last blocks, entry states, invalid profiles
-    in the long and the short half, every stereo format, and mono streams
-    (split only with VARIANT_SPLITW) in the same batch."""
-    rng = np.random.default_rng(11)
+def test_batch_streams_share_k1_workgroups(built):
+    """Streams of one or two waves each, so every K1 workgroup holds waves
+    of several streams and formats: its inner-boundary verification must
+    check a wave's first chunk against the previous wave only when both are
+    the same stream.  Warm-up 0 with chunks of 16 forces repairs and
+    cascades inside workgroups and across their boundaries (K2); entry
+    states, cut last blocks and an invalid profile ride along."""
+    rng = np.random.default_rng(21)
     specs = []
-    for i, eb in enumerate([4096, 4096, 4000, 3900, 4096, 4095]):
-        bits = (8, 6, 4)[i % 3]
-        cut = 7 if i == 3 else 0
+    for i in range(40):
+        bits, ch = FORMATS[i % 6]
+        eb = int(rng.integers(40, 2048))
+        cut = int(rng.integers(1, 32)) if i % 5 == 0 else 0
         state = tuple(int(v) for v in rng.integers(-3000, 3000, 4))
-        specs.append(make(eb, bits, 2, 700 + i, mix="W" if i == 4 else "A", cut=cut,
-                          state=state))
-    for i, blk in enumerate([300 * 2 + 1, 3500 * 2]):      # long half, short half
-        xa, eb, bits, ch, frames, state = make(4096, 8, 2, 720 + i)
-        xa = xa.copy()
-        xa[blk * 33] = 0x5F
-        specs.append((xa, eb, bits, ch, frames, state))
-    specs.append(make(8192, 8, 1, 730))
-    specs.append(make(8192, 4, 1, 731, cut=3))
-    pcms, st = run_batch(specs, chunk=64, variant=variant)
+        specs.append(make(eb, bits, ch, 800 + i, mix="W" if i % 3 == 0 else "A",
+                          cut=cut, state=state))
+    xa, eb, bits, ch, frames, state = specs[7]
+    xa = xa.copy()
+    xa[(eb // 2) * ch * (bits * 4 + 1)] = 0x5F
+    specs[7] = (xa, eb, bits, ch, frames, state)
+    pcms, st = run_batch(specs, chunk=16, warmup=0)
     check(specs, pcms, st)
-    # the exact-fit stereo streams ran split: status reports the short chunk
-    assert st[0][6] == 28 and st[1][6] == 28
-    assert st[0][7] == (12 if variant == bjxa_amd.VARIANT_SPLIT else 16)
-
-
-def test_batch_split_off_matches(built):
-    """The same batch with and without the split (one chunk length by
-    default) gives the same PCM and states."""
-    specs = [make(4096, 8, 2, 740 + i) for i in range(4)]
-    a, sa = run_batch(specs, chunk=64, variant=bjxa_amd.VARIANT_SPLIT)
-    b, sb = run_batch(specs, chunk=64)
-    check(specs, a, sa)
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y)
-    assert (sa[:, :3] == sb[:, :3]).all()
-    assert sa[0][6] == 28 and sb[0][6] == 32
+    assert st[:, 3].sum() > 0

@@ -32,19 +32,18 @@ def test_worst_case_mix_full_size(built):
 
 
 @pytest.mark.parametrize("bits,ch", [(8, 2), (8, 1), (4, 2), (6, 1)])
-def test_balanced_plan_ragged(built, bits, ch):
-    """The two-length chunk plan (VARIANT_BALANCED) splits a long stream into
-    exactly 512 x 256 chunks (the long ones first, whole waves).  A ragged
-    length, a cut last block and a 2-eblock warm-up (so many chunks need
-    repair across long/short boundaries) must still be bit-exact."""
+def test_auto_plan_short_warmup(built, bits, ch):
+    """The automatic plan on a ragged stream with a cut last block and a
+    2-eblock warm-up, so many chunks need repair: inside K1 workgroups
+    (verified and repaired by K1 itself) and at their boundaries (K2)."""
     eb = 2_500_003
     frames = eb * 32 - 7
     xa = synth.stream(eb, bits, ch, "A", seed=5)
     ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, (1, -2, 3, -4), frames)
     got, st = dev_decode(xa, eb, bits, ch, frames=frames, state=(1, -2, 3, -4),
-                         warmup=2, want_status=True, variant=bjxa_amd.VARIANT_BALANCED)
+                         warmup=2, want_status=True)
     assert np.array_equal(got, ref)
-    assert st[5] == 131067 and st[3] > 0
+    assert st[3] > 0
     assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
 
 

@@ -1,0 +1,68 @@
+#!/bin/bash
+# One GPU-box session (replaces the per-experiment gpu_r3*.sh launchers):
+#   bash tools/gpu_run.sh <tag> <step> [<step> ...]
+# Steps, run in order; the first failure ends the session (no GPU work
+# after a fault, a time limit or a crash):
+#   tests[=<pytest -k expr>]  pytest -m gpu (all, or the selected tests)
+#   smoke                     __graft_entry__.smoke()
+#   bench[=<args>]            python bench.py <args>, line -> <tag>_bench.json
+#   ab=<wl>:<mix>[:<reps>[:<names>]]  tools/ab_inproc.py: this tree's library
+#                             against ab/<name>/libbjxa.so.0 for each name of the
+#                             comma list (default: every ab/*), interleaved in one
+#                             process
+#   prof[=<args>]             tools/profile.sh <tag> <args> (trace + counter passes)
+# Logs under gpurun_out/<tag>_*.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+T=$1
+shift
+mkdir -p gpurun_out
+fail() { echo "FAILED: $1"; [ -f "$2" ] && tail -30 "$2"; exit 1; }
+for step in "$@"; do
+	name=${step%%=*}
+	arg=
+	[ "$name" != "$step" ] && arg=${step#*=}
+	case $name in
+	tests)
+		log=gpurun_out/${T}_gpu.log
+		if [ -n "$arg" ]; then
+			timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+			    --timeout-method thread -k "$arg" > $log 2>&1 || fail tests $log
+		else
+			timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+			    --timeout-method thread > $log 2>&1 || fail tests $log
+		fi
+		tail -1 $log ;;
+	smoke)
+		log=gpurun_out/${T}_smoke.log
+		timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ||
+		    fail smoke $log
+		tail -1 $log ;;
+	bench)
+		out=gpurun_out/${T}_bench.json
+		# shellcheck disable=SC2086
+		timeout -k 10 600 python bench.py $arg > $out 2> gpurun_out/${T}_bench.err ||
+		    fail bench gpurun_out/${T}_bench.err
+		python3 tools/bench_brief.py $out ;;
+	ab)
+		IFS=: read -r wl mix reps names <<< "$arg"
+		log=gpurun_out/${T}_ab_${wl}_${mix}${names:+_${names//,/_}}.log
+		libs="new=bjxa_amd/libbjxa.so.0"
+		for d in ab/*/; do
+			n=$(basename "$d")
+			[ -n "$names" ] && [[ ",$names," != *",$n,"* ]] && continue
+			[ -f "$d/libbjxa.so.0" ] && libs="$libs $n=$d/libbjxa.so.0"
+		done
+		# shellcheck disable=SC2086
+		timeout -k 10 600 python tools/ab_inproc.py --wl "$wl" --mix "${mix:-A}" \
+		    --reps "${reps:-6}" $libs > $log 2>&1 || fail ab $log
+		cat $log ;;
+	prof)
+		# shellcheck disable=SC2086
+		bash tools/profile.sh "$T" $arg || exit 1
+		python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["kernel_us_alone"], d.get("traffic"))' \
+		    gpurun_out/prof_$T/summary.json ;;
+	*)
+		fail "unknown step $step" ;;
+	esac
+done
