@@ -52,6 +52,7 @@ struct xa_dec_args {
 				 * same wave, nchunks entries (batches: the
 				 * batch's list, global chunk indices) */
 	uint32_t *nlist;	/* its length (ctl[XA_CTL_NL] of the launch) */
+	uint32_t lcap;		/* its capacity in entries */
 	uint32_t lbase;		/* list entry = lbase + chunk (batches: the
 				 * stream's first global chunk) */
 	uint32_t *ctl;		/* XA_CTL_WORDS */

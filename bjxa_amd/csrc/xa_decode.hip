@@ -56,7 +56,7 @@
 #ifndef XA_FIX_PF
 #define XA_FIX_PF 4		/* repair windows in flight per lane */
 #endif
-#define XA_FIX_THREADS 512	/* K2: one workgroup boundary per thread */
+#define XA_FIX_THREADS 256	/* K2 workgroup size */
 
 static_assert(XA_SCTL_FIXED == XA_CTL_FIXED && XA_SCTL_ERR == XA_CTL_ERR,
     "a batch stream's control words double as xa_dec_args::ctl");
@@ -64,6 +64,20 @@ static_assert(XA_SCTL_FIXED == XA_CTL_FIXED && XA_SCTL_ERR == XA_CTL_ERR,
 /* bytes of PCM per lane per store phase: one stereo eblock, two mono */
 #define XA_LB 128
 #define XA_NST 16	/* store instructions per group (G * OB / 16) */
+
+/* one 16-B piece of PCM, streamed out: non-temporal (the line stays in the
+ * XCD's L2 until evicted), or with XA_PCM_SC1 system-coherent write-through
+ * (MI355X_MICROARCH.md: sc1 stores leave L2 at once and drop the line) */
+__device__ __forceinline__ void
+pcm_store(uint8_t *p, const u32x4a v)
+{
+#ifdef XA_PCM_SC1
+	asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) :
+	    "memory");
+#else
+	__builtin_nontemporal_store(v, (u32x4a *)p);
+#endif
+}
 
 /*
  * Store the wave's staged XA_LB-byte lines: line j belongs to chunk
@@ -87,7 +101,7 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 #pragma unroll
 		for (int i = 0; i < P; i++) {
 			const u32x4a v = *(const u32x4a *)(lbase + i * LPI * LINE);
-			__builtin_nontemporal_store(v, (u32x4a *)(gp + i * istride));
+			pcm_store(gp + i * istride, v);
 		}
 		return;
 	}
@@ -103,7 +117,7 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 			const u32x4a v = *(const u32x4a *)(lbase + i * LPI * LINE);
 			uint8_t *q = gp + i * istride;
 			if (q + 16 <= end)
-				__builtin_nontemporal_store(v, (u32x4a *)q);
+				pcm_store(q, v);
 		}
 		return;
 	}
@@ -169,9 +183,19 @@ stage_half(const xa_dec_args &a, uint8_t *land, int lane, int64_t wstart,
 	typedef geo2<BITS, CH> g2;
 	const int64_t c0 = wstart + (int64_t)h * 32 * Cw;
 	const int64_t e_first = c0 + rel;
+#ifdef XA_DBG_LINE_RUNS
+	/* the diagnostic's own footprint: runs at whole-line strides reach
+	 * further than the real ones */
+	const bool inside = e_first >= 0 && (int64_t)(((size_t)c0 * g::EBSZ) &
+	    ~(size_t)127) + (rel + (int64_t)a.W) / (2 * g::G) * 256 +
+	    32 * (int64_t)((Cw * g::EBSZ + 127u) & ~127u) <=
+	    (int64_t)a.eblocks * g::EBSZ;
+#else
 	const int64_t e_end = c0 + 31 * (int64_t)Cw + rel + 2 * g::G;
-	if (e_first >= 0 && e_end * g::EBSZ + (g2::SLOT - 4 * g2::RD) <=
-	    (int64_t)a.eblocks * g::EBSZ) {
+	const bool inside = e_first >= 0 && e_end * g::EBSZ +
+	    (g2::SLOT - 4 * g2::RD) <= (int64_t)a.eblocks * g::EBSZ;
+#endif
+	if (inside) {
 #ifdef XA_DBG_LINE_RUNS
 		/* diagnostic build only (wrong output): every run is two whole
 		 * 128-B lines, runs of a lane back to back (no line is fetched
@@ -263,9 +287,23 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 	auto fetch = [&](uint32_t *r, int64_t b) {
 		const int64_t d0 = (b * EBSZ) >> 2;
 		if constexpr (BUF) {
+			/* dwords 0 .. NIN-1 hold only bytes of eblock b (whatever
+			 * its alignment), so 16-B loads there never straddle the
+			 * range check; the rest one dword at a time */
+			constexpr int NIN = (EBSZ - 1) / 4 + 1, N4 = NIN / 4;
 			const uint32_t o = (uint32_t)d0 * 4u;
 #pragma unroll
-			for (int i = 0; i <= WN; i++)
+			for (int i = 0; i < N4; i++) {
+				const u32x4a v = __builtin_bit_cast(u32x4a,
+				    __builtin_amdgcn_raw_buffer_load_b128(rs,
+				    (int)(o + 16u * i), 0, 0));
+				r[4 * i] = v.x;
+				r[4 * i + 1] = v.y;
+				r[4 * i + 2] = v.z;
+				r[4 * i + 3] = v.w;
+			}
+#pragma unroll
+			for (int i = 4 * N4; i <= WN; i++)
 				r[i] = __builtin_amdgcn_raw_buffer_load_b32(rs,
 				    (int)(o + 4u * i), 0, 0);
 		} else {
@@ -370,6 +408,9 @@ __device__ __forceinline__ void
 list_mismatches(const xa_dec_args &a, int lane, uint32_t q, bool live, uint2 gs,
     uint2 ex)
 {
+#ifdef XA_DBG_LINE_RUNS
+	return;		/* diagnostic build: no K2, so nothing would drain a list */
+#endif
 	const uint32_t px = __shfl_up(ex.x, 1), py = __shfl_up(ex.y, 1);
 	const bool mism = live && lane > 0 && q < a.nchunks &&
 	    (px != gs.x || py != gs.y);
@@ -380,9 +421,14 @@ list_mismatches(const xa_dec_args &a, int lane, uint32_t q, bool live, uint2 gs,
 	if (lane == 0)
 		base = atomicAdd(a.nlist, (uint32_t)__builtin_popcountll(bal));
 	base = __shfl(base, 0);
-	if (mism)
-		a.list[base + (uint32_t)__builtin_popcountll(bal &
-		    ((1ull << lane) - 1ull))] = a.lbase + q;
+	/* each chunk is listed at most once per launch and K2 empties the
+	 * list, so it never holds more than lcap entries; the bound only keeps
+	 * a workspace left inconsistent by a failed launch from being written
+	 * past */
+	const uint32_t j = base + (uint32_t)__builtin_popcountll(bal &
+	    ((1ull << lane) - 1ull));
+	if (mism && j < a.lcap)
+		a.list[j] = a.lbase + q;
 }
 
 /* ------------------------------------------------------------------ */
@@ -518,6 +564,9 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 			uint32_t bad = decode_eblock<BITS, CH, true, true, LB,
 			    u * 4 * CH>(r, hh * 4 * GDW + u * EBSZ, p0, p1, line,
 			    flush);
+#ifdef XA_DBG_LINE_RUNS	/* (its garbage profiles would all contend here) */
+			bad = 0;
+#endif
 			if (act && bad) {
 				uint32_t cb = (uint32_t)b * CH + ((bad & 1u) ? 0u : 1u);
 				atomicMin(&a.ctl[XA_CTL_ERR], cb);
@@ -791,6 +840,22 @@ k2_entry(const uint32_t *list, uint32_t nb, uint32_t i)
 }
 
 /*
+ * This thread's first entry of K2's grid-stride loop.  Entries are dealt
+ * round-robin over the workgroups first, then over the waves of each, then
+ * over the lanes: the listed mismatches are contiguous, and given to
+ * consecutive lanes they would pile dozens of serial repairs onto a few
+ * waves of a few CUs (a repaired block costs ~1 us on a lone lane but ~4 us
+ * with four busy waves on one CU, DESIGN.md §5 round 2 exp. 11).
+ */
+__device__ __forceinline__ uint32_t
+k2_first()
+{
+	constexpr uint32_t WPB = XA_FIX_THREADS / 64;
+	return ((threadIdx.x & 63u) * WPB + (threadIdx.x >> 6)) * gridDim.x +
+	    blockIdx.x;
+}
+
+/*
  * K2 for one stream.  Each thread takes entries of the check list in a
  * grid-stride loop: chunk q is compared with its predecessor's exit and
  * repaired on a mismatch; a repair that does not meet the stored
@@ -808,11 +873,10 @@ xa_decode_fix(xa_dec_args a)
 	const uint64_t *e64 = (const uint64_t *)a.e;
 	const uint64_t *g64 = (const uint64_t *)a.g;
 	const uint32_t nb = (n + 63u) / 64u - 1u;
-	const uint32_t total = nb + *a.nlist;
+	const uint32_t total = nb + min(*a.nlist, a.lcap);
 	bool wrote = false;
 	uint32_t nfix = 0;
-	for (uint32_t i = blockIdx.x * XA_FIX_THREADS + threadIdx.x; i < total;
-	    i += gridDim.x * XA_FIX_THREADS) {
+	for (uint32_t i = k2_first(); i < total; i += gridDim.x * XA_FIX_THREADS) {
 		const uint32_t q = k2_entry(a.list, nb, i);
 		/* e[q-1] may be rewritten concurrently by chunk q-1's fixer;
 		 * whichever value is read is recorded in g[q], and that fixer
@@ -841,15 +905,17 @@ xa_decode_fix(xa_dec_args a)
 }
 
 /* K2's grid: enough threads for every wave boundary plus a list of up to
- * a quarter of the chunks in one pass, at most XA_FIX_MAXWG workgroups (a
- * longer list takes more passes of the grid-stride loop) */
+ * half the chunks in one pass, at most XA_FIX_MAXWG workgroups -- about one
+ * per CU, so that dense repairs (mix W: a quarter of the chunks) spread
+ * over the whole chip; a longer list takes more passes of the grid-stride
+ * loop */
 #ifndef XA_FIX_MAXWG
-#define XA_FIX_MAXWG 128u
+#define XA_FIX_MAXWG 256u
 #endif
 static unsigned
 k2_grid(uint64_t nwaves, uint64_t nchunks)
 {
-	const uint64_t want = nwaves - 1 + nchunks / 4;
+	const uint64_t want = nwaves - 1 + nchunks / 2;
 	uint64_t g = (want + XA_FIX_THREADS - 1) / XA_FIX_THREADS;
 	if (g < 1)
 		g = 1;
@@ -953,6 +1019,7 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.e = b.e + d.cbase;
 	a.queue = b.queue;
 	a.list = b.list;
+	a.lcap = 64u * b.nwaves;
 	a.nlist = &b.ctl[XA_CTL_NL];
 	a.lbase = d.cbase;
 	a.ctl = b.sctl + sid * XA_SCTL_WORDS;	/* ERR and FIXED line up */
@@ -1089,10 +1156,9 @@ xa_decode_fix_batch(xa_batch_args b)
 	const uint64_t *e64 = (const uint64_t *)b.e;
 	const uint64_t *g64 = (const uint64_t *)b.g;
 	const uint32_t nb = b.nwaves - 1u;
-	const uint32_t total = nb + b.ctl[XA_CTL_NL];
+	const uint32_t total = nb + min(b.ctl[XA_CTL_NL], 64u * b.nwaves);
 	bool wrote = false;
-	for (uint32_t i = blockIdx.x * XA_FIX_THREADS + threadIdx.x; i < total;
-	    i += gridDim.x * XA_FIX_THREADS) {
+	for (uint32_t i = k2_first(); i < total; i += gridDim.x * XA_FIX_THREADS) {
 		const uint32_t Q = k2_entry(b.list, nb, i);
 		const uint32_t sid = b.wstream[Q / 64];
 		const xa_batch_stream &d = b.streams[sid];

@@ -211,6 +211,7 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.queue = (uint32_t *)(a.e + p.nchunks);
 	a.list = a.queue + 2 * (size_t)p.nchunks;
 	a.nlist = &a.ctl[XA_CTL_NL];
+	a.lcap = p.nchunks;
 	a.lbase = 0;
 	a.status = d_status;
 	hipEvent_t e0 = tune ? (hipEvent_t)tune->ev_spec[0] : NULL;

@@ -11,6 +11,11 @@
 #                             comma list (default: every ab/*), interleaved in one
 #                             process
 #   prof[=<args>]             tools/profile.sh <tag> <args> (trace + counter passes)
+#   ktrace=<wl>:<mix>:<names> rocprofv3 --kernel-trace over tools/ab_inproc.py, one
+#                             run per library (new = this tree's, else ab/<name>/):
+#                             per-kernel median and mean durations of each
+#   pmc=<wl>:<mix>:<names>    the same with rocprofv3 --pmc TCC_EA0_RDREQ_sum
+#                             TCC_EA0_WRREQ_sum (own pass): bytes per dispatch
 # Logs under gpurun_out/<tag>_*.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -62,6 +67,32 @@ for step in "$@"; do
 		bash tools/profile.sh "$T" $arg || exit 1
 		python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["kernel_us_alone"], d.get("traffic"))' \
 		    gpurun_out/prof_$T/summary.json ;;
+	ktrace)
+		IFS=: read -r wl mix names <<< "$arg"
+		for n in ${names//,/ }; do
+			lib=ab/$n/libbjxa.so.0
+			[ "$n" = new ] && lib=bjxa_amd/libbjxa.so.0
+			d=$PWD/gpurun_out/${T}_kt_${wl}_${mix}_$n
+			mkdir -p "$d"
+			( export TMPDIR=/tmp; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace \
+			    --stats --output-format csv -d "$d" -o run -- python3 \
+			    "$OLDPWD/tools/ab_inproc.py" --wl "$wl" --mix "$mix" --reps 3 \
+			    "$n=$OLDPWD/$lib" > "$d/log" 2>&1 ) || fail ktrace "$d/log"
+			python3 tools/kstats.py "$d/run_kernel_trace.csv" "$n $wl $mix"
+		done ;;
+	pmc)
+		IFS=: read -r wl mix names <<< "$arg"
+		for n in ${names//,/ }; do
+			lib=ab/$n/libbjxa.so.0
+			[ "$n" = new ] && lib=bjxa_amd/libbjxa.so.0
+			d=$PWD/gpurun_out/${T}_pmc_${wl}_${mix}_$n
+			mkdir -p "$d"
+			( export TMPDIR=/tmp; cd /tmp && timeout -s KILL 120 rocprofv3 --pmc \
+			    TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --output-format csv -d "$d" -o run \
+			    -- python3 "$OLDPWD/tools/ab_inproc.py" --wl "$wl" --mix "$mix" \
+			    --reps 1 --steps 5 "$n=$OLDPWD/$lib" > "$d/log" 2>&1 ) || fail pmc "$d/log"
+			python3 tools/pmc_brief.py "$d" "$n $wl $mix"
+		done ;;
 	*)
 		fail "unknown step $step" ;;
 	esac
