@@ -287,6 +287,8 @@ def encode_wav(data, bits=6):
 # ---- device-resident extension (include/bjxa_hip.h) ----------------------
 
 VARIANT_PACE_OFF = 15 << 8   # tuning variant bits 8-11: no pacing barriers
+VARIANT_DECOR = 0x10000      # batches: the longer chunks of packed PCM images, forced
+VARIANT_NODECOR = 0x20000    # batches: the same, never
 
 
 def decode_workspace_size(eblocks, channels, chunk=0, warmup=-1, variant=0):

@@ -11,7 +11,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <utility>
+#include <vector>
 
 #include "xa_decode.h"
 #include "xa_gpu.h"
@@ -297,6 +300,60 @@ stream_ok(const bjxa_hip_stream_t *s)
 }
 
 /*
+ * Streams whose PCM images are carved out of one large device allocation
+ * (as bjxa_hip_decode_files does, or a caller packing a batch into one
+ * buffer) lie in one physically contiguous run, and there a chunk length
+ * whose PCM lane stride is a multiple of 8 KiB lines every lane of every
+ * stream up on the same HBM channels: C5's per-GPU share at 8 GPUs (64
+ * eblocks = 8 KiB) runs 0.43 ms packed against 0.30 ms in allocations of
+ * their own, whatever the VA gaps between the streams (DESIGN.md §5 round 2
+ * exp. 14, R3-7).  Such streams get chunks one quantum longer.  Streams in
+ * allocations of their own do not pay the penalty (even where a caching
+ * allocator puts two in one segment), and there the longer chunks would
+ * only cost time (round 2 exp. 16), so the planner asks the runtime which
+ * allocation each PCM image belongs to and lengthens the chunks of streams
+ * that share one with at least XA_PACKED_MIN others.  Tuning variant bit 16
+ * forces the longer chunks for every stream, bit 17 forbids them.
+ */
+#define XA_VARIANT_DECOR	0x10000u
+#define XA_VARIANT_NODECOR	0x20000u
+#define XA_PACKED_MIN		8u
+
+static void
+packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t,
+    std::vector<uint8_t> &packed)
+{
+	const uint32_t v = t ? t->variant : 0u;
+	packed.assign(n, (v & XA_VARIANT_DECOR) ? 1 : 0);
+	if (v & (XA_VARIANT_DECOR | XA_VARIANT_NODECOR) || n < XA_PACKED_MIN)
+		return;
+	std::vector<std::pair<uintptr_t, uint32_t>> base(n);
+	bool failed = false;
+	for (uint32_t i = 0; i < n; i++) {
+		hipDeviceptr_t b = NULL;
+		size_t sz = 0;
+		if (hipMemGetAddressRange(&b, &sz, (hipDeviceptr_t)s[i].d_dst) !=
+		    hipSuccess) {
+			b = NULL;	/* not a device allocation we can see */
+			failed = true;
+		}
+		base[i] = { (uintptr_t)b, i };
+	}
+	if (failed)
+		(void)hipGetLastError();	/* not the caller's error */
+	std::sort(base.begin(), base.end());
+	for (uint32_t i = 0; i < n;) {
+		uint32_t j = i;
+		while (j < n && base[j].first == base[i].first)
+			j++;
+		if (base[i].first != 0 && j - i >= XA_PACKED_MIN)
+			for (uint32_t k = i; k < j; k++)
+				packed[base[k].second] = 1;
+		i = j;
+	}
+}
+
+/*
  * Plan: one budget of channel blocks per lane, Cb = the batch's channel
  * blocks / target_lanes() (at least MIN_CHUNK, a multiple of 4); a stream of
  * E eblocks and ch channels gets k = round(E*ch / (64*Cb)) >= 1 whole
@@ -349,6 +406,8 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	    DEFAULT_WARMUP;
 	const uint32_t W = (w + 7) & ~7u;	/* a whole chunk quantum of every format */
 
+	std::vector<uint8_t> packed;
+	packed_pcm(s, n, tune, packed);
 	xa_batch_stream *hs = (xa_batch_stream *)calloc(n, sizeof *hs);
 	if (hs == NULL) {
 		errno = ENOMEM;
@@ -365,6 +424,8 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		if (c < MIN_CHUNK)
 			c = MIN_CHUNK;
 		c = (c + G - 1) / G * G;
+		if (packed[i] && (c * 64u * ch) % 8192u == 0)
+			c += G;
 		const uint32_t nch = (uint32_t)((E + c - 1) / c);
 		hs[i].src = (const uint8_t *)s[i].d_src;
 		hs[i].dst = (uint8_t *)s[i].d_dst;

@@ -47,8 +47,11 @@ typedef struct {
 	uint32_t	variant;	/* bits 8-11: pacing of the speculative
 					 * kernel's waves (0 = automatic, 15 =
 					 * off, n = a barrier every n groups);
-					 * other bits reserved (0).  Pass the
-					 * same tuning to
+					 * batches: bit 16 forces, bit 17
+					 * forbids the longer chunks planned
+					 * for packed PCM images (automatic:
+					 * by layout); other bits reserved
+					 * (0).  Pass the same tuning to
 					 * bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 

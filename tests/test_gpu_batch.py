@@ -178,3 +178,44 @@ def test_batch_streams_share_k1_workgroups(built):
     pcms, st = run_batch(specs, chunk=16, warmup=0)
     check(specs, pcms, st)
     assert st[:, 3].sum() > 0
+
+
+def run_packed(specs, chunk, packed, variant=0):
+    """run_batch with every stream's XA and PCM carved from one allocation
+    each, back to back (packed), or in allocations of their own."""
+    torch = require_gpu()
+    sizes = [eb * 64 * ch for _, eb, _, ch, _, _ in specs]
+    if packed:
+        big = torch.full((sum(sizes),), 0x5A, dtype=torch.uint8, device="cuda")
+        offs = np.cumsum([0] + sizes[:-1])
+        dsts = [big[o:o + n] for o, n in zip(offs, sizes)]
+    else:
+        dsts = [torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda") for n in sizes]
+    srcs = [torch.from_numpy(np.ascontiguousarray(xa)).cuda() for xa, *_ in specs]
+    streams = [{"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb, "bits": bits,
+                "channels": ch, "frames": frames, "state": state}
+               for s, d, (xa, eb, bits, ch, frames, state) in zip(srcs, dsts, specs)]
+    status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    with bjxa_amd.Batch(streams, chunk, -1, sh, variant) as b:
+        b.decode(status.data_ptr(), sh)
+        torch.cuda.synchronize()
+    out = [d.cpu().numpy().view(np.int16)[:frames * ch].copy()
+           for d, (_, _, _, ch, frames, _) in zip(dsts, specs)]
+    return out, status.cpu().numpy().view(np.uint32).reshape(len(specs), -1).copy()
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_batch_packed_layout_plan(built, packed):
+    """Streams whose PCM lane stride is a multiple of 8 KiB (here 64 stereo
+    eblocks per lane) get chunks one quantum longer when their PCM images
+    are packed back to back in one allocation, and keep them otherwise;
+    bit-exact either way, including with the choice forced off and on."""
+    specs = [make(4096, 8, 2, 900 + i, cut=(5 if i == 3 else 0)) for i in range(8)]
+    pcms, st = run_packed(specs, 128, packed)
+    check(specs, pcms, st)
+    assert (st[:, 6] == (68 if packed else 64)).all()
+    for v, c in ((bjxa_amd.VARIANT_NODECOR, 64), (bjxa_amd.VARIANT_DECOR, 68)):
+        pcms, st = run_packed(specs, 128, packed, v)
+        check(specs, pcms, st)
+        assert (st[:, 6] == c).all()

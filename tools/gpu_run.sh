@@ -10,6 +10,7 @@
 #                             against ab/<name>/libbjxa.so.0 for each name of the
 #                             comma list (default: every ab/*), interleaved in one
 #                             process
+#   abx=<args>                tools/ab_inproc.py <args> as given (layouts, tunings)
 #   prof[=<args>]             tools/profile.sh <tag> <args> (trace + counter passes)
 #   ktrace=<wl>:<mix>:<names> rocprofv3 --kernel-trace over tools/ab_inproc.py, one
 #                             run per library (new = this tree's, else ab/<name>/):
@@ -61,6 +62,11 @@ for step in "$@"; do
 		# shellcheck disable=SC2086
 		timeout -k 10 600 python tools/ab_inproc.py --wl "$wl" --mix "${mix:-A}" \
 		    --reps "${reps:-6}" $libs > $log 2>&1 || fail ab $log
+		cat $log ;;
+	abx)
+		log=gpurun_out/${T}_abx_$(echo "$arg" | tr -c 'A-Za-z0-9' _ | cut -c1-60).log
+		# shellcheck disable=SC2086
+		timeout -k 10 600 python tools/ab_inproc.py $arg > $log 2>&1 || fail abx $log
 		cat $log ;;
 	prof)
 		# shellcheck disable=SC2086
