@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 FORMATS = [(8, 2), (6, 2), (4, 2), (8, 1), (6, 1), (4, 1)]
 
 
-def run_batch(specs, chunk=0, warmup=-1, repeat=1):
+def run_batch(specs, chunk=0, warmup=-1, repeat=1, variant=0):
     """specs: list of (xa bytes, eblocks, bits, ch, frames, state).  Returns
     (pcm list, status array [n, 8])."""
     torch = require_gpu()
@@ -28,7 +28,7 @@ def run_batch(specs, chunk=0, warmup=-1, repeat=1):
                         "bits": bits, "channels": ch, "frames": frames, "state": state})
     status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    with bjxa_amd.Batch(streams, chunk, warmup, sh) as b:
+    with bjxa_amd.Batch(streams, chunk, warmup, sh, variant) as b:
         for _ in range(repeat):
             b.decode(status.data_ptr(), sh)
         torch.cuda.synchronize()
@@ -60,7 +60,12 @@ def make(eb, bits, ch, seed, mix="A", cut=0, state=(0, 0, 0, 0)):
     return (xa, eb, bits, ch, eb * 32 - cut, state)
 
 
-def test_batch_mixed_formats(built):
+@pytest.mark.parametrize("variant", [0, bjxa_amd.VARIANT_DECOR])
+def test_batch_mixed_formats(built, variant):
+    """Every format, ragged lengths, cut last blocks, entry states; with
+    VARIANT_DECOR every stream also gets the packed-layout plan (chunks one
+    quantum longer where the stride is on 8 KiB, a chunk grid shifted by a
+    per-stream phase)."""
     rng = np.random.default_rng(3)
     specs = []
     for i in range(48):
@@ -69,16 +74,18 @@ def test_batch_mixed_formats(built):
         cut = int(rng.integers(0, 32)) if i % 4 == 0 else 0
         state = tuple(int(v) for v in rng.integers(-3000, 3000, 4))
         specs.append(make(eb, bits, ch, 100 + i, cut=cut, state=state))
-    pcms, st = run_batch(specs)
+    pcms, st = run_batch(specs, variant=variant)
     check(specs, pcms, st)
 
 
-def test_batch_repairs_and_cascades(built):
+@pytest.mark.parametrize("variant", [0, bjxa_amd.VARIANT_DECOR])
+def test_batch_repairs_and_cascades(built, variant):
     """Warm-up 0 and short chunks: nearly every chunk is repaired and
-    worst-case profiles cascade through whole chunks."""
+    worst-case profiles cascade through whole chunks (with and without the
+    phase-shifted chunk grids of the packed-layout plan)."""
     specs = [make(30000, bits, ch, 200 + i, mix="W" if i % 2 else "A")
              for i, (bits, ch) in enumerate(FORMATS)]
-    pcms, st = run_batch(specs, chunk=16, warmup=0)
+    pcms, st = run_batch(specs, chunk=16, warmup=0, variant=variant)
     check(specs, pcms, st)
     assert st[:, 3].sum() > 0
 
