@@ -136,9 +136,13 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 		if (cj >= nch)
 			continue;
 		const uint8_t *from = obuf + j * LINE + pc * 16;
-		if (off + 16u <= lim) {
+		/* off < lim first: a piece before a phased stream's start has
+		 * off = 2^64 - 16k, and off + 16 would wrap for k = 1 */
+		if (off >= lim)
+			continue;
+		if (lim - off >= 16u) {
 			*(u32x4a *)(dst + off) = *(const u32x4a *)from;
-		} else if (off < lim) {
+		} else {
 			for (uint64_t k = 0; off + k < lim; k += 2)
 				*(uint16_t *)(dst + off + k) =
 				    *(const uint16_t *)(from + k);
