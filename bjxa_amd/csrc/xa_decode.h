@@ -40,11 +40,8 @@ struct xa_dec_args {
 	uint32_t eblocks;
 	uint32_t nchunks;
 	uint32_t C, W;		/* chunk and warm-up lengths in eblocks
-				 * (multiples of XA_CHUNK_Q(ch)); chunk q >= 1
-				 * starts at eblock q*C - phase */
-	uint32_t phase;		/* chunk 0 is [0, C - phase) (batches of
-				 * packed streams; 0 otherwise), phase < C,
-				 * a multiple of XA_CHUNK_Q(ch) */
+				 * (multiples of XA_CHUNK_Q(ch)); chunk q
+				 * starts at eblock q*C */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
 	uint32_t pace;		/* K1 waves of a workgroup wait for each other
 				 * every `pace` groups (0 = never) */
@@ -83,8 +80,7 @@ struct xa_batch_stream {		/* 64 B, device table entry */
 	uint32_t C;			/* chunk length, eblocks */
 	uint32_t init[2];
 	uint32_t fmt;			/* bits | channels << 8 */
-	uint32_t phase;			/* as xa_dec_args::phase */
-	uint32_t pad[2];
+	uint32_t pad[3];
 };
 
 /* per-stream control words (xa_batch_args::sctl); ERR and FIXED sit where

@@ -136,8 +136,7 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 		if (cj >= nch)
 			continue;
 		const uint8_t *from = obuf + j * LINE + pc * 16;
-		/* off < lim first: a piece before a phased stream's start has
-		 * off = 2^64 - 16k, and off + 16 would wrap for k = 1 */
+		/* (off < lim first, so that no bound can wrap) */
 		if (off >= lim)
 			continue;
 		if (lim - off >= 16u) {
@@ -269,7 +268,7 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 	if (CH == 2)
 		xa_unpack_state(s.y, p0[CH - 1], p1[CH - 1]);
 	const int64_t eblocks = a.eblocks;
-	const int64_t b0 = (int64_t)q * a.C - a.phase;	/* q >= 1 */
+	const int64_t b0 = (int64_t)q * a.C;
 	int64_t b1 = b0 + a.C;
 	if (b1 > eblocks)
 		b1 = eblocks;
@@ -467,9 +466,7 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 	uint8_t *land = region, *ost = region + g2::HALF;
 	const int64_t eblocks = a.eblocks;
 	const uint32_t Cw = a.C;
-	/* with a phase the grid starts `phase` eblocks before the stream: the
-	 * first wave's lane 0 skips those (no decode, no store) */
-	const int64_t wstart = (int64_t)wchunk0 * Cw - a.phase;
+	const int64_t wstart = (int64_t)wchunk0 * Cw;
 	const int64_t b0 = wstart + (int64_t)lane * Cw;
 	const int W = (int)a.W;
 	/* super-steps: NW of warm-up, then NC of the chunk (W and Cw are
@@ -507,11 +504,9 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 	const uint8_t *lbase = ost + (lane / P) * LINE + (lane % P) * 16;
 	uint8_t *line = ost + lane * LINE;
 	const uint64_t full_blocks = a.pcm_bytes / OB;
-	const bool wave_full = wstart >= 0 && wchunk0 + 63u < a.nchunks &&
+	const bool wave_full = wchunk0 + 63u < a.nchunks &&
 	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
-	/* a wave that starts before the stream takes the per-piece stores,
-	 * whose bounds skip the pieces before it */
-	const bool clean = wstart >= 0 && (a.pcm_bytes & 15u) == 0;
+	const bool clean = (a.pcm_bytes & 15u) == 0;
 	auto none = [](int) {};
 
 	/* copy this lane's run out of the landing buffer (half h only) */
@@ -562,7 +557,7 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 				__builtin_amdgcn_s_setprio(0);
 				wave_lds_sync();
 			};
-			const bool act = (uint64_t)b < (uint64_t)eblocks;
+			const bool act = b < eblocks;
 			int32_t q0[CH], q1[CH];
 #pragma unroll
 			for (int c = 0; c < CH; c++) {
@@ -1019,7 +1014,6 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.eblocks = d.eblocks;
 	a.nchunks = d.nchunks;
 	a.C = d.C;
-	a.phase = d.phase;
 	a.W = b.W;
 	a.pace = 0;	/* the batch kernel decides per workgroup */
 	a.init[0] = d.init[0];

@@ -197,7 +197,6 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.eblocks = s->eblocks;
 	a.nchunks = p.nchunks;
 	a.C = p.C;
-	a.phase = 0;
 	a.W = p.W;
 	a.pace = pick_pace((p.W + p.C) / XA_CHUNK_Q(s->channels), false, tune);
 	a.init[0] = ((uint32_t)(uint16_t)s->state[0]) |
@@ -313,29 +312,19 @@ stream_ok(const bjxa_hip_stream_t *s)
  * allocator puts two in one segment), and there the longer chunks would
  * only cost time (round 2 exp. 16), so the planner asks the runtime which
  * allocation each PCM image belongs to and lengthens the chunks of streams
- * that share one with at least XA_PACKED_MIN others.  Those streams also
- * shift their chunk grids against each other: stream j of the allocation
- * gets a chunk 0 shorter by phase = Q * (j mod 16) eblocks, so its lanes'
- * PCM sits 512-B steps away from its neighbours' instead of at the same
- * offset modulo the streams' spacing; the phase is used only where it adds
- * no wave (the longer chunks leave the slack).  Tuning variant bit 16
- * forces both for every stream, bit 17 forbids them.
+ * that share one with at least XA_PACKED_MIN others.  Tuning variant bit 16
+ * forces the longer chunks for every stream, bit 17 forbids them.
  */
 #define XA_VARIANT_DECOR	0x10000u
 #define XA_VARIANT_NODECOR	0x20000u
 #define XA_PACKED_MIN		8u
 
-/* packed[i]: 0, or 1 + stream i's rank (mod 16) among the streams packed
- * into its allocation (the phase of its chunk grid) */
 static void
 packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t,
     std::vector<uint8_t> &packed)
 {
 	const uint32_t v = t ? t->variant : 0u;
-	packed.assign(n, 0);
-	if (v & XA_VARIANT_DECOR)
-		for (uint32_t i = 0; i < n; i++)
-			packed[i] = (uint8_t)(1u + i % 16u);
+	packed.assign(n, (v & XA_VARIANT_DECOR) ? 1 : 0);
 	if (v & (XA_VARIANT_DECOR | XA_VARIANT_NODECOR) || n < XA_PACKED_MIN)
 		return;
 	std::vector<std::pair<uintptr_t, uint32_t>> base(n);
@@ -359,7 +348,7 @@ packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t,
 			j++;
 		if (base[i].first != 0 && j - i >= XA_PACKED_MIN)
 			for (uint32_t k = i; k < j; k++)
-				packed[base[k].second] = (uint8_t)(1u + (k - i) % 16u);
+				packed[base[k].second] = 1;
 		i = j;
 	}
 }
@@ -437,20 +426,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		c = (c + G - 1) / G * G;
 		if (packed[i] && (c * 64u * ch) % 8192u == 0)
 			c += G;
-		uint32_t nch = (uint32_t)((E + c - 1) / c);
-		/* packed streams also shift their chunk grids against each
-		 * other (chunk 0 shorter by phase), where that adds no wave */
-		uint32_t phase = 0;
-		if (packed[i]) {
-			const uint32_t m = (uint32_t)(c / G) < 16u ? (uint32_t)(c / G) : 16u;
-			const uint32_t ph = G * (packed[i] - 1u) % (G * m);
-			const uint32_t n2 = (uint32_t)((E + ph + c - 1) / c);
-			if ((n2 + 63) / 64 == (nch + 63) / 64) {
-				phase = ph;
-				nch = n2;
-			}
-		}
-		hs[i].phase = phase;
+		const uint32_t nch = (uint32_t)((E + c - 1) / c);
 		hs[i].src = (const uint8_t *)s[i].d_src;
 		hs[i].dst = (uint8_t *)s[i].d_dst;
 		hs[i].pcm_bytes = s[i].frames * 2u * ch;

@@ -64,8 +64,7 @@ def make(eb, bits, ch, seed, mix="A", cut=0, state=(0, 0, 0, 0)):
 def test_batch_mixed_formats(built, variant):
     """Every format, ragged lengths, cut last blocks, entry states; with
     VARIANT_DECOR every stream also gets the packed-layout plan (chunks one
-    quantum longer where the stride is on 8 KiB, a chunk grid shifted by a
-    per-stream phase)."""
+    quantum longer where the stride is on 8 KiB)."""
     rng = np.random.default_rng(3)
     specs = []
     for i in range(48):
@@ -82,7 +81,7 @@ def test_batch_mixed_formats(built, variant):
 def test_batch_repairs_and_cascades(built, variant):
     """Warm-up 0 and short chunks: nearly every chunk is repaired and
     worst-case profiles cascade through whole chunks (with and without the
-    phase-shifted chunk grids of the packed-layout plan)."""
+    packed-layout plan)."""
     specs = [make(30000, bits, ch, 200 + i, mix="W" if i % 2 else "A")
              for i, (bits, ch) in enumerate(FORMATS)]
     pcms, st = run_batch(specs, chunk=16, warmup=0, variant=variant)
