@@ -872,6 +872,9 @@ template <int BITS, int CH, bool BUF>
 __global__ __launch_bounds__(XA_FIX_THREADS) void
 xa_decode_fix(xa_dec_args a)
 {
+#ifdef XA_DBG_K2_EMPTY
+	return;		/* diagnostic build: the kernel boundary alone */
+#endif
 	const uint32_t n = a.nchunks;
 	const uint64_t *e64 = (const uint64_t *)a.e;
 	const uint64_t *g64 = (const uint64_t *)a.g;
@@ -902,8 +905,15 @@ xa_decode_fix(xa_dec_args a)
 	}
 	if (nfix)
 		atomicAdd(&a.ctl[XA_CTL_FIXED], nfix);
+#ifdef XA_DBG_K2_NOTICKET
+	/* diagnostic build: workgroup 0 drains without waiting for the others */
+	(void)wrote;
+	if (blockIdx.x != 0 || threadIdx.x != 0)
+		return;
+#else
 	if (!k2_last(&a.ctl[XA_CTL_TICKET], wrote) || threadIdx.x != 0)
 		return;
+#endif
 	drain_tail<BITS, CH, BUF>(a);
 }
 
