@@ -287,13 +287,16 @@ def timed_region(step, steps, depth, slots, dev):
     return elapsed, ms
 
 
-def spread(ms):
+def spread(ms, depth=1):
     """min / median / max of per-step event times (ms)"""
     if not ms:
         return None
+    what = "hipEvents around each step of the timed region, on its stream"
+    if depth > 1:
+        what += ("; %d steps in flight, so each span also holds the overlapping steps' "
+                 "share of the chip (ms_per_step is the throughput)" % depth)
     return {"min": round(float(np.min(ms)), 4), "median": round(float(np.median(ms)), 4),
-            "max": round(float(np.max(ms)), 4), "n": len(ms),
-            "what": "hipEvents around each step of the timed region, on its stream"}
+            "max": round(float(np.max(ms)), 4), "n": len(ms), "what": what}
 
 
 PIPE_CAL_STEPS = 20     # steps per calibration run of --pipeline 0
@@ -425,7 +428,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     xa_bytes = eb * ch * (bits * 4 + 1)
     return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
             "elapsed": elapsed, "serial": serial, "pipeline": depth, "pipeline_cal": cal,
-            "step_ms": spread(step_ms), "spec_ms": float(np.median(spec_ms)),
+            "step_ms": spread(step_ms, depth), "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
             "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
 
@@ -636,7 +639,7 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
             "samples": samples, "elapsed": elapsed,
             "value": round(samples * steps / elapsed / 1e6, 1) if elapsed else 0.0,
             "unit": "MSamples/s",
-            "ms_per_step": round(elapsed / steps * 1e3, 4), "step_ms": spread(step_ms),
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "step_ms": spread(step_ms, depth),
             "pipeline": depth, "pipeline_cal": cal,
             "ms_per_step_serial": round(serial / steps * 1e3, 4),
             "spec_ms": round(spec_ms, 4), "spec_samples": len(spec),
