@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--eblocks", type=int, default=0,
                     help="single-stream workloads: override the stream length")
     ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps", "gaps2m",
-                                                        "skew"],
+                                                        "skew", "pages"],
                     help="batches: one allocation per stream buffer (sep) or all "
                          "streams back to back in one allocation (packed)")
     ap.add_argument("builds", nargs="+")
@@ -75,11 +75,12 @@ def main():
         else:
             inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)),
                                         mix=args.mix)
-        if args.layout in ("packed", "gaps", "gaps2m", "skew"):
+        if args.layout in ("packed", "gaps", "gaps2m", "skew", "pages"):
             # every stream in one allocation, back to back at 256-B steps
             # (gaps: plus a seeded random gap of 0-255 x 256 B before each;
             # gaps2m: 0-31 x 64 KiB; skew: stream i at +(37 i mod 32) x
-            # 64 KiB + (i mod 16) x 4 KiB)
+            # 64 KiB + (i mod 16) x 4 KiB; pages: each stream on a fresh 2 MiB
+            # boundary after 0-3 whole 2 MiB pages left unused)
             rng = np.random.default_rng(7)
 
             def carve(sizes):
@@ -89,6 +90,9 @@ def main():
                         o += int(rng.integers(0, 256)) * 256
                     elif args.layout == "gaps2m":
                         o += int(rng.integers(0, 32)) * 65536
+                    elif args.layout == "pages":
+                        o = (o + (1 << 21) - 1) // (1 << 21) * (1 << 21) + \
+                            int(rng.integers(0, 4)) * (1 << 21)
                     elif args.layout == "skew":
                         o = (o + (1 << 21) - 1) // (1 << 21) * (1 << 21) + \
                             ((37 * k) % 32) * 65536 + (k % 16) * 4096
