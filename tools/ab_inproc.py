@@ -53,7 +53,8 @@ def main():
     ap.add_argument("--eblocks", type=int, default=0,
                     help="single-stream workloads: override the stream length")
     ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps", "gaps2m",
-                                                        "skew", "pages"],
+                                                        "skew", "pages", "packed_src",
+                                                        "packed_dst"],
                     help="batches: one allocation per stream buffer (sep) or all "
                          "streams back to back in one allocation (packed)")
     ap.add_argument("builds", nargs="+")
@@ -75,7 +76,8 @@ def main():
         else:
             inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)),
                                         mix=args.mix)
-        if args.layout in ("packed", "gaps", "gaps2m", "skew", "pages"):
+        if args.layout in ("packed", "gaps", "gaps2m", "skew", "pages", "packed_src",
+                           "packed_dst"):
             # every stream in one allocation, back to back at 256-B steps
             # (gaps: plus a seeded random gap of 0-255 x 256 B before each;
             # gaps2m: 0-31 x 64 KiB; skew: stream i at +(37 i mod 32) x
@@ -100,10 +102,19 @@ def main():
                     o += (n + 255) // 256 * 256
                 big = torch.empty(o, dtype=torch.uint8, device="cuda")
                 return [big[a:a + n] for a, n in zip(offs, sizes)]
-            srcs = carve([x.size for *_, x in inputs])
-            for t_, (*_, x) in zip(srcs, inputs):
-                t_.copy_(torch.from_numpy(x))
-            dsts = carve([eb * 64 * ch for _, _, ch, eb, _ in inputs])
+            # (packed_src / packed_dst: only the XA inputs / only the PCM
+            # images back to back in one allocation, the other side separate)
+            if args.layout == "packed_dst":
+                srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
+            else:
+                srcs = carve([x.size for *_, x in inputs])
+                for t_, (*_, x) in zip(srcs, inputs):
+                    t_.copy_(torch.from_numpy(x))
+            if args.layout == "packed_src":
+                dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+                        for _, _, ch, eb, _ in inputs]
+            else:
+                dsts = carve([eb * 64 * ch for _, _, ch, eb, _ in inputs])
         else:
             srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
             dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
