@@ -26,6 +26,25 @@ WL = {"C3": (5_000_000, 8, 2), "C2": (10_000_000, 8, 1), "C3s": (1_000_000, 8, 2
 BATCH = ("C4", "C5", "C5g")
 
 
+_HIP = []
+
+
+def raw_buffer(n):
+    """A uint8 CUDA tensor over a hipMalloc of exactly n bytes (kept for the
+    life of the process)."""
+    if not _HIP:
+        h = ctypes.CDLL("libamdhip64.so.7")
+        h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        _HIP.append(h)
+    p = ctypes.c_void_p()
+    assert _HIP[0].hipMalloc(ctypes.byref(p), n) == 0
+
+    class Iface:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": "|u1",
+                                    "data": (p.value, False), "version": 2}
+    return torch.as_tensor(Iface(), device="cuda")
+
+
 def load(path):
     L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL)
     L.bjxa_hip_decode_workspace.restype = ctypes.c_size_t
@@ -54,7 +73,7 @@ def main():
                     help="single-stream workloads: override the stream length")
     ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps", "gaps2m",
                                                         "skew", "pages", "packed_src",
-                                                        "packed_dst"],
+                                                        "packed_dst", "hipmalloc"],
                     help="batches: one allocation per stream buffer (sep) or all "
                          "streams back to back in one allocation (packed)")
     ap.add_argument("builds", nargs="+")
@@ -115,6 +134,13 @@ def main():
                         for _, _, ch, eb, _ in inputs]
             else:
                 dsts = carve([eb * 64 * ch for _, _, ch, eb, _ in inputs])
+        elif args.layout == "hipmalloc":
+            # every buffer a hipMalloc of its own at its exact size (as a C
+            # caller would make them), outside torch's caching allocator
+            srcs = [raw_buffer(x.size) for *_, x in inputs]
+            for t_, (*_, x) in zip(srcs, inputs):
+                t_.copy_(torch.from_numpy(x))
+            dsts = [raw_buffer(eb * 64 * ch) for _, _, ch, eb, _ in inputs]
         else:
             srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
             dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
