@@ -64,6 +64,7 @@ gloo (tests/test_gpu_bench.py drives it at 2 and 3 ranks).
 import argparse
 import contextlib
 import ctypes
+import datetime
 import json
 import os
 import socket
@@ -94,6 +95,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 CPU_PASSES = 5
 EV_SAMPLES = 20         # launches timed with events, after the timed region
 NO_ERROR = 0xFFFFFFFF
+# every collective (and the rendezvous) of a rank gives up after this long, so
+# a stuck rank ends the job with its rank named instead of hanging for
+# torch's default 10 minutes
+PG_TIMEOUT_S = float(os.environ.get("BJXA_BENCH_PG_TIMEOUT", "180"))
 FIRST_ERR_NONE = (1 << 62)
 
 
@@ -103,6 +108,19 @@ def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def init_pg(backend, **kw):
+    """Join the job's process group with PG_TIMEOUT_S on every collective."""
+    import torch.distributed as dist
+    dist.init_process_group(backend, timeout=datetime.timedelta(seconds=PG_TIMEOUT_S), **kw)
+
+
+def stall_for_test(rank):
+    """tests/test_dist.py: BJXA_BENCH_STALL_RANK=r makes rank r sleep
+    BJXA_BENCH_STALL_S seconds before its first collective (a stuck rank)."""
+    if os.environ.get("BJXA_BENCH_STALL_RANK", "") == str(rank):
+        time.sleep(float(os.environ.get("BJXA_BENCH_STALL_S", "60")))
 
 
 def launch_ranks(n):
@@ -259,31 +277,37 @@ def timed_serial(step, steps, dev):
 
 def timed_region(step, steps, depth, slots, dev):
     """The timed region: `steps` steps (consecutive slots when depth > 1,
-    else slot 0), bracketed by a barrier (N > 1) and device synchronizes.
-    Each step is also bracketed by hipEvents recorded on its slot's stream,
-    so the line can show the spread of the steps inside the window.
-    Returns (wall seconds, per-step event ms)."""
+    else slot 0), bracketed by a barrier (N > 1) and device synchronizes,
+    and nothing else on the streams.  Then the same steps once more with a
+    hipEvent pair recorded around each on its slot's stream, untimed, for
+    the spread of the steps: an event between two steps costs the step
+    after it ~4 % on C3 (tools/window_probe.py), which is
+    why round 4's timed window, which held them, ran slower than the same
+    loop without them.  Returns (wall seconds, per-step event ms)."""
     import torch
     import torch.distributed as dist
-    evs = EventPairs(steps)
-    rec = evs.hip.hipEventRecord
     torch.cuda.synchronize(dev)
     if dist_on():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(steps):
+        step(i if depth > 1 else 0)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist_on():
+        dist.barrier()
+    evs = EventPairs(steps)
+    rec = evs.hip.hipEventRecord
+    for i in range(steps):
         k = i if depth > 1 else 0
         sh = slots[k % len(slots)]["sh"]
         rec(evs.ev[i][0], sh)
         step(k)
         rec(evs.ev[i][1], sh)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist_on():
-        dist.barrier()
     ms = evs.ms()
     evs.close()
+    torch.cuda.synchronize(dev)
     return elapsed, ms
 
 
@@ -291,7 +315,9 @@ def spread(ms, depth=1):
     """min / median / max of per-step event times (ms)"""
     if not ms:
         return None
-    what = "hipEvents around each step of the timed region, on its stream"
+    what = ("hipEvents around each step of a pass of the same steps right after the "
+            "timed region (outside it: an event between steps slows the next one), "
+            "on its stream")
     if depth > 1:
         what += ("; %d steps in flight, so each span also holds the overlapping steps' "
                  "share of the chip (ms_per_step is the throughput)" % depth)
@@ -836,7 +862,7 @@ def main():
     if backend == "gloo":
         dev = torch.device("cpu")
         if world > 1 or args.force_pg:
-            dist.init_process_group("gloo")
+            init_pg("gloo")
         return main_c5_cpu(args, dev, world, rank)
     if backend == "gloo-gpu":
         # rehearsal of the N > 1 GPU path on a one-GPU box: every rank
@@ -844,7 +870,7 @@ def main():
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         if world > 1:
-            dist.init_process_group("gloo")
+            init_pg("gloo")
         try:
             return main_c5(args, dev, world, rank, cdev=torch.device("cpu"))
         finally:
@@ -859,7 +885,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or args.force_pg:
-        dist.init_process_group("nccl", device_id=dev)
+        init_pg("nccl", device_id=dev)
     try:
         if workload == "C5":
             return main_c5(args, dev, world, rank)
@@ -1085,6 +1111,7 @@ def main_c5_cpu(args, dev, world, rank):
     specs = batch_specs("C5", nstreams, eblocks)
     lo, hi = shard_range(len(specs), rank, world)
     inputs = batch_inputs("C5", nstreams, eblocks, lo, hi, args.bad_stream)
+    stall_for_test(rank)
     if dist_on():
         dist.barrier()
     t0 = time.perf_counter()
@@ -1143,5 +1170,16 @@ def main_c5_cpu(args, dev, world, rank):
     return 0 if ok in (None, True) else 1
 
 
+def main_named():
+    """main(), with a failure of this rank (a collective that timed out, a
+    peer that died) reported under its rank before the exit status."""
+    try:
+        return main()
+    except Exception as e:  # noqa: BLE001 -- report, then fail the job
+        print("bench.py rank %s: %s: %s" % (os.environ.get("RANK", "0"), type(e).__name__, e),
+              file=sys.stderr, flush=True)
+        return 3
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main_named())

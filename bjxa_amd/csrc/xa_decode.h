@@ -7,12 +7,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+/* xa_dec_args::flags, test knobs of the verify pass (tuning variant bits
+ * 18 and 19, include/bjxa_hip.h) */
+#define XA_F_NORECORD	1u	/* no exit records: every wave's first boundary
+				 * goes to the sequential tail */
+#define XA_SPIN_TICKS	20000u	/* default xa_dec_args::spin (200 us); tuning
+				 * variant bit 19 sets 0 */
+
 /* workspace control words (reset by the tail kernel after every call) */
 #define XA_CTL_ERR	0	/* min channel-block index with gain >= 5 */
-#define XA_CTL_NQ	1	/* re-check queue length */
-#define XA_CTL_FIXED	2	/* chunks repaired by K2 */
-#define XA_CTL_TICKET	3	/* K2 workgroups finished (last one runs the tail) */
-#define XA_CTL_NL	4	/* chunks K1 listed for K2 (inner-wave mismatches) */
+#define XA_CTL_NQ	1	/* entries appended to the re-check queue */
+#define XA_CTL_FIXED	2	/* chunks repaired */
+#define XA_CTL_OVF	3	/* the queue overflowed (a workspace left
+				 * inconsistent by a failed launch): the tail
+				 * re-checks every chunk boundary */
 #define XA_CTL_WORDS	64	/* 256 B */
 
 /* status words written by the tail kernel */
@@ -45,22 +53,30 @@ struct xa_dec_args {
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
 	uint32_t pace;		/* K1 waves of a workgroup wait for each other
 				 * every `pace` groups (0 = never) */
-	uint2 *g, *e;		/* per-chunk entry / exit state */
-	uint32_t *queue;	/* re-check queue, 2 * nchunks entries */
-	uint32_t *list;		/* K1 -> K2: chunks whose entry differs from
-				 * the exit of the chunk before them in the
-				 * same wave, nchunks entries (batches: the
-				 * batch's list, global chunk indices) */
-	uint32_t *nlist;	/* its length (ctl[XA_CTL_NL] of the launch) */
-	uint32_t lcap;		/* its capacity in entries */
-	uint32_t lbase;		/* list entry = lbase + chunk (batches: the
-				 * stream's first global chunk) */
+	uint2 *g, *e;		/* per-chunk entry / exit state, as repaired */
+	uint32_t *queue;	/* chunks for the tail to re-check in order
+				 * (entry = qbase + chunk; batches: the batch's
+				 * queue, global chunk indices) */
+	uint32_t *nq;		/* its length (ctl[XA_CTL_NQ] of the launch) */
+	uint32_t qcap;		/* its capacity in entries */
+	uint32_t qbase;		/* the stream's first global chunk */
+	uint32_t *ovf;		/* ctl[XA_CTL_OVF] of the launch */
+	uint4 *exits;		/* per wave of the stream: the exit state its
+				 * last chunk left, tagged (xa_decode.hip) */
+	uint32_t tag;		/* this launch's record tag, never 0 */
+	uint32_t spin;		/* 100-MHz ticks a wave waits for the record
+				 * of the wave before it */
+	uint32_t flags;		/* XA_F_* */
 	uint32_t *ctl;		/* XA_CTL_WORDS */
 	uint32_t *status;	/* XA_ST_WORDS */
 };
 
-/* K1 (decode, verify inside each workgroup) and K2 (boundaries between
- * K1 workgroups, cascades, status) on `st`; ev0/ev1 (optional) around K1 */
+/*
+ * The decode kernel (decode, verify and repair every chunk boundary it can
+ * see, including the one with the previous wave) and the tail kernel
+ * (cascades and what the first could not settle, in chunk order; status) on
+ * `st`; ev0/ev1 (optional) around the first.
+ */
 hipError_t xa_decode_launch(const xa_dec_args &a, unsigned bits, unsigned ch,
     hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 
@@ -98,8 +114,9 @@ struct xa_batch_args {
 	uint32_t pace;			/* as xa_dec_args::pace */
 	uint2 *g, *e;			/* per global chunk */
 	uint32_t *queue;		/* 2 * 64 * nwaves */
-	uint32_t *list;			/* 64 * nwaves (xa_dec_args::list) */
-	uint32_t *ctl;			/* XA_CTL_WORDS (NQ, TICKET, NL) */
+	uint4 *exits;			/* per global wave (xa_dec_args::exits) */
+	uint32_t tag, spin, flags;	/* as xa_dec_args */
+	uint32_t *ctl;			/* XA_CTL_WORDS (NQ, OVF) */
 	uint32_t *sctl;			/* XA_SCTL_WORDS per stream */
 	uint32_t *status;		/* XA_ST_WORDS per stream */
 };

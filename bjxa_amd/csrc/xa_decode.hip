@@ -14,23 +14,25 @@
  *  K1 xa_decode_spec  each lane warms up over the W eblocks before its chunk
  *                     starting from state (0,0) -- exact if a gain-0 block
  *                     occurs there, and two trajectories that meet stay
- *                     together -- then decodes its chunk, emitting PCM.  It
- *                     records g[q] (state it entered the chunk with) and e[q]
- *                     (state it left with).  Chunk 0 starts from the true
- *                     caller state and needs no warm-up.  Chunk q is correct
- *                     iff chunk q-1 is and g[q] == e[q-1]; each wave checks
- *                     that for its 63 inner boundaries (a lane shuffle) and
- *                     lists the chunks that differ.
- *  K2 xa_decode_fix   re-checks every wave's first chunk and the listed
- *                     ones (so its work follows the mismatches, not the
- *                     stream length); each mismatching chunk re-decodes from
- *                     e[q-1] block by block until its block-end state meets
- *                     the stored trajectory (everything after is then
- *                     unchanged).  A chunk that never meets it rewrites e[q]
- *                     and queues q+1.  The last workgroup to finish (arrival
- *                     ticket) drains that queue in chunk order with one
- *                     thread, so a cascade through several chunks is
- *                     repaired exactly.
+ *                     together -- then decodes its chunk, emitting PCM.
+ *                     Chunk 0 starts from the true caller state and needs
+ *                     no warm-up.  Chunk q is correct iff chunk q-1 is and
+ *                     its entry state equals q-1's exit.  Each wave then
+ *                     settles its own boundaries: its last lane publishes
+ *                     its exit for the next wave (a tagged record), every
+ *                     lane compares its entry with the exit of the chunk
+ *                     before it (a lane shuffle; lane 0 reads the previous
+ *                     wave's record), and each mismatching chunk is
+ *                     re-decoded by its own lane from the true entry, block
+ *                     by block, until its block-end state meets the stored
+ *                     trajectory (everything after is then unchanged).  A
+ *                     chunk that never meets it, or a record that does not
+ *                     come in time, queues a chunk for K2.  The repairs run
+ *                     on the CU that wrote the PCM, beside the waves still
+ *                     decoding, not after the whole grid.
+ *  K2 xa_decode_tail  one workgroup: drains that queue in chunk order with
+ *                     one thread, so a cascade through several chunks is
+ *                     repaired exactly, and publishes the status.
  *
  * By induction from chunk 0 every chunk ends up decoded from its true start
  * state: the output is bit-exact for any input; speculation only sets the
@@ -56,7 +58,7 @@
 #ifndef XA_FIX_PF
 #define XA_FIX_PF 4		/* repair windows in flight per lane */
 #endif
-#define XA_FIX_THREADS 256	/* K2 workgroup size */
+#define XA_TAIL_THREADS 256	/* K2 workgroup size */
 
 static_assert(XA_SCTL_FIXED == XA_CTL_FIXED && XA_SCTL_ERR == XA_CTL_ERR,
     "a batch stream's control words double as xa_dec_args::ctl");
@@ -242,23 +244,25 @@ stage_half(const xa_dec_args &a, uint8_t *land, int lane, int64_t wstart,
  * the f32 chain), so repaired PCM is K1's arithmetic bit for bit.  Stops
  * once a block-end state equals the stored trajectory (frames 30/31 of the
  * old PCM) in every channel: nothing after it can change.  Returns true if
- * it met the trajectory; otherwise stores the chunk's new exit state in
- * e[q] and returns it in `exit`.
+ * it met the trajectory; otherwise returns the chunk's new exit state in
+ * `exit` (the caller records it).
  *
  * The repair is one serial chain per chunk, so its time is its instruction
  * count (~11 VALU per frame, ~1 us per block alone).
  *
  * No load sits under a branch (hipcc drains vmcnt(0) right after such
  * loads): the windows and old end states of the blocks XA_FIX_PF ahead are
- * fetched every iteration with clamped addresses.  BUF (a wave-uniform
- * stream under 4 GiB of XA): the window comes through a buffer descriptor
- * of the stream, whose range check returns 0 past the end, instead of
- * per-dword 64-bit clamps (the stream's descriptor is the same for every
- * lane, so BUF needs it to be uniform: one stream per launch).
+ * fetched every iteration with clamped addresses.  The windows come through
+ * a buffer descriptor whose base is eblock `bb` of the stream (bb <= the
+ * chunk's first eblock, the same for every active lane: the wave's first
+ * eblock in K1, the chunk's own in the one-thread tail) and whose range
+ * ends with the stream, so its range check returns 0 past the end instead
+ * of per-dword 64-bit clamps.  The planner keeps a wave's span of XA under
+ * 4 GiB (xa_gpu.hip), so every offset fits the descriptor's 32 bits.
  */
-template <int BITS, int CH, bool BUF = false>
+template <int BITS, int CH>
 __device__ __forceinline__ bool
-fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
+fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit, int64_t bb)
 {
 	typedef geo<BITS, CH> g;
 	constexpr int EBSZ = g::EBSZ, OB = g::OB;
@@ -272,48 +276,45 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 	int64_t b1 = b0 + a.C;
 	if (b1 > eblocks)
 		b1 = eblocks;
-	const int64_t ndw = (eblocks * EBSZ + 3) / 4;
-	const uint32_t *src = (const uint32_t *)a.src;
 	/* q >= 1, so the stream has whole blocks (nfull >= b0 >= 16) */
 	const int64_t nfull = (int64_t)(a.pcm_bytes / OB);
 
+	/* the descriptor: base at eblock bb's dword, range to the stream's end
+	 * (at most 2^32 - 256 bytes) */
+	const uint64_t base_b = ((uint64_t)bb * EBSZ) & ~(uint64_t)3;
+	const uint64_t span = ((uint64_t)eblocks * EBSZ + 3u) / 4u * 4u - base_b;
 	__amdgpu_buffer_rsrc_t rs;
-	if constexpr (BUF) {
-		const uint64_t sp = (uint64_t)a.src;
+	{
+		const uint64_t sp = (uint64_t)a.src + base_b;
 		const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)sp);
 		const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(sp >> 32));
-		const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)(ndw * 4));
+		const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)min(span,
+		    (uint64_t)0xffffff00u));
 		rs = __builtin_amdgcn_make_buffer_rsrc(
 		    (void *)(((uint64_t)hi << 32) | lo), 0, (int)nb, 0x00020000);
 	}
 	/* the WN + 1 dwords holding eblock b */
 	auto fetch = [&](uint32_t *r, int64_t b) {
-		const int64_t d0 = (b * EBSZ) >> 2;
-		if constexpr (BUF) {
-			/* dwords 0 .. NIN-1 hold only bytes of eblock b (whatever
-			 * its alignment), so 16-B loads there never straddle the
-			 * range check; the rest one dword at a time */
-			constexpr int NIN = (EBSZ - 1) / 4 + 1, N4 = NIN / 4;
-			const uint32_t o = (uint32_t)d0 * 4u;
+		/* dwords 0 .. NIN-1 hold only bytes of eblock b (whatever its
+		 * alignment), so 16-B loads there never straddle the range
+		 * check; the rest one dword at a time */
+		constexpr int NIN = (EBSZ - 1) / 4 + 1, N4 = NIN / 4;
+		const uint32_t o = (uint32_t)((((uint64_t)b * EBSZ) & ~(uint64_t)3) -
+		    base_b);
 #pragma unroll
-			for (int i = 0; i < N4; i++) {
-				const u32x4a v = __builtin_bit_cast(u32x4a,
-				    __builtin_amdgcn_raw_buffer_load_b128(rs,
-				    (int)(o + 16u * i), 0, 0));
-				r[4 * i] = v.x;
-				r[4 * i + 1] = v.y;
-				r[4 * i + 2] = v.z;
-				r[4 * i + 3] = v.w;
-			}
-#pragma unroll
-			for (int i = 4 * N4; i <= WN; i++)
-				r[i] = __builtin_amdgcn_raw_buffer_load_b32(rs,
-				    (int)(o + 4u * i), 0, 0);
-		} else {
-#pragma unroll
-			for (int i = 0; i <= WN; i++)
-				r[i] = src[min(d0 + i, ndw - 1)];
+		for (int i = 0; i < N4; i++) {
+			const u32x4a v = __builtin_bit_cast(u32x4a,
+			    __builtin_amdgcn_raw_buffer_load_b128(rs,
+			    (int)(o + 16u * i), 0, 0));
+			r[4 * i] = v.x;
+			r[4 * i + 1] = v.y;
+			r[4 * i + 2] = v.z;
+			r[4 * i + 3] = v.w;
 		}
+#pragma unroll
+		for (int i = 4 * N4; i <= WN; i++)
+			r[i] = __builtin_amdgcn_raw_buffer_load_b32(rs,
+			    (int)(o + 4u * i), 0, 0);
 	};
 	/* old end state of block b: its PCM frames 30 and 31 as stored (raw, so
 	 * nothing uses the loaded words before the block's compare, PF blocks
@@ -392,46 +393,136 @@ fix_chunk(const xa_dec_args &a, uint32_t q, uint2 s, uint2 &exit)
 		return true;
 	exit.x = xa_pack_state(p0[0], p1[0]);
 	exit.y = CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u;
-	a.e[q] = exit;
 	return false;
 }
 
 /*
- * K1's inner-wave check, after its main loop (no barrier, no LDS): lane l
- * holds chunk q (stream-local) with entry state gs and exit state ex; its
- * predecessor q-1 is lane l-1 of the same wave (lane 0's belongs to the
- * previous wave, which K2 checks).  Chunk q is correct iff q-1 is and gs
- * equals q-1's exit, so every lane whose entry differs from its
- * neighbour's exit appends lbase + q to the list K2 repairs from (one
- * atomic per wave).  A repair that changes q-1's exit makes K2 re-check q
- * in its sequential tail, so checking against the speculative exits here
- * is exact.
+ * The exit record a wave leaves for the next one: lane 63's exit state as
+ * two 8-B granules {state, launch tag}, each written by one agent-scope
+ * atomic store and read by agent-scope atomic loads (write-through and
+ * L1-bypassing: the placement-independent granule hand-off of
+ * MI355X_MICROARCH.md, which needs no fence), so a reader sees either this
+ * launch's record or one it recognises as not yet written (a torn read
+ * fails the tag of one half).  Nothing else passes between waves: each wave
+ * repairs only the PCM it wrote itself.
  */
 __device__ __forceinline__ void
-list_mismatches(const xa_dec_args &a, int lane, uint32_t q, bool live, uint2 gs,
-    uint2 ex)
+put_exit(uint4 *rec, uint2 ex, uint32_t tag)
 {
-#ifdef XA_DBG_LINE_RUNS
-	return;		/* diagnostic build: no K2, so nothing would drain a list */
-#endif
-	const uint32_t px = __shfl_up(ex.x, 1), py = __shfl_up(ex.y, 1);
-	const bool mism = live && lane > 0 && q < a.nchunks &&
-	    (px != gs.x || py != gs.y);
-	const uint64_t bal = __ballot(mism);
-	if (bal == 0)
-		return;
-	uint32_t base = 0;
-	if (lane == 0)
-		base = atomicAdd(a.nlist, (uint32_t)__builtin_popcountll(bal));
-	base = __shfl(base, 0);
-	/* each chunk is listed at most once per launch and K2 empties the
-	 * list, so it never holds more than lcap entries; the bound only keeps
-	 * a workspace left inconsistent by a failed launch from being written
-	 * past */
-	const uint32_t j = base + (uint32_t)__builtin_popcountll(bal &
-	    ((1ull << lane) - 1ull));
-	if (mism && j < a.lcap)
-		a.list[j] = a.lbase + q;
+	uint64_t *p = (uint64_t *)rec;
+	__hip_atomic_store(p, (uint64_t)ex.x | (uint64_t)tag << 32,
+	    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	__hip_atomic_store(p + 1, (uint64_t)ex.y | (uint64_t)tag << 32,
+	    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool
+get_exit(const uint4 *rec, uint32_t tag, uint2 &ex)
+{
+	const uint64_t *p = (const uint64_t *)rec;
+	const uint64_t lo = __hip_atomic_load(p, __ATOMIC_RELAXED,
+	    __HIP_MEMORY_SCOPE_AGENT);
+	const uint64_t hi = __hip_atomic_load(p + 1, __ATOMIC_RELAXED,
+	    __HIP_MEMORY_SCOPE_AGENT);
+	ex = make_uint2((uint32_t)lo, (uint32_t)hi);
+	return (uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag;
+}
+
+/* queue stream chunk q for K2's in-order re-check; past the queue's
+ * capacity (only a workspace left inconsistent by a failed launch gets
+ * there) K2 re-checks every boundary instead, so nothing is dropped */
+__device__ __forceinline__ void
+enqueue(const xa_dec_args &a, uint32_t q)
+{
+	const uint32_t j = atomicAdd(a.nq, 1u);
+	if (j < a.qcap)
+		a.queue[j] = a.qbase + q;
+	else
+		atomicOr(a.ovf, 1u);
+}
+
+/*
+ * After K1's main loop: the wave settles the boundaries of its 64 chunks.
+ * Lane l holds stream chunk q = wchunk0 + l with entry state gs and exit
+ * state ex.  Chunk q is correct iff q-1 is and gs equals q-1's exit: lane
+ * l-1's (a shuffle), or for lane 0 the previous wave's record, which lane
+ * 63 of that wave published right after its main loop.  Every mismatching
+ * lane re-decodes its own chunk from that exit (fix_chunk, one serial chain
+ * per lane, all of the wave's repairs side by side); a repair that does not
+ * meet the stored trajectory changes q's exit and queues q+1 for K2, so
+ * checking against the speculative exits is exact.  If the previous wave's
+ * record is not there at once, the wave first does its other repairs, then
+ * lane 0 polls for up to `a.spin` ticks (an exit condition every wave
+ * reaches: nothing here waits on a workgroup that might not be resident);
+ * a record that does not come queues q itself for K2.  Finally each lane
+ * records the entry it was decoded from and its exit (g[q], e[q]) for K2.
+ */
+template <int BITS, int CH>
+__device__ __forceinline__ void
+settle_wave(const xa_dec_args &a, int lane, uint32_t wchunk0, uint2 gs, uint2 ex)
+{
+	const uint32_t q = wchunk0 + (uint32_t)lane, n = a.nchunks;
+	const bool live = q < n;
+	const uint32_t wl = wchunk0 / 64u;	/* the wave within its stream */
+	const bool norec = (a.flags & XA_F_NORECORD) != 0u;
+	if (lane == 63 && q + 1u < n && !norec)
+		put_exit(&a.exits[wl], ex, a.tag);
+	uint2 s = make_uint2(__shfl_up(ex.x, 1), __shfl_up(ex.y, 1));
+	bool wait = live && lane == 0 && wchunk0 > 0;
+	bool chk = live && lane > 0;
+	if (wait && norec) {
+		enqueue(a, q);
+		wait = false;
+	}
+	if (wait && get_exit(&a.exits[wl - 1], a.tag, s)) {
+		wait = false;
+		chk = true;
+	}
+	/* the wave's own PCM stores are complete before repairs read them */
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	uint2 g = gs, e = ex;
+	bool fixed = false;
+#pragma nounroll
+	for (int round = 0; round < 2; round++) {
+		if (round == 1) {
+			if (__ballot(wait) == 0)
+				break;
+			if (wait) {
+				const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+				bool got;
+				while (!(got = get_exit(&a.exits[wl - 1], a.tag, s)) &&
+				    __builtin_amdgcn_s_memrealtime() - t0 < a.spin)
+					__builtin_amdgcn_s_sleep(2);
+				if (got)
+					chk = true;
+				else
+					enqueue(a, q);
+			}
+		}
+		const bool fix = chk && (s.x != gs.x || s.y != gs.y);
+		chk = false;
+		if (__ballot(fix) == 0)
+			continue;
+		if (fix) {
+			uint2 nx;
+			const bool met = fix_chunk<BITS, CH>(a, q, s, nx,
+			    (int64_t)wchunk0 * a.C);
+			g = s;
+			fixed = true;
+			if (!met) {
+				e = nx;
+				if (q + 1u < n)
+					enqueue(a, q + 1u);
+			}
+		}
+	}
+	const uint64_t nf = __ballot(fixed);
+	if (nf != 0 && lane == 0)
+		atomicAdd(&a.ctl[XA_CTL_FIXED], (uint32_t)__builtin_popcountll(nf));
+	if (live) {
+		a.g[q] = g;
+		a.e[q] = e;
+	}
 }
 
 /* ------------------------------------------------------------------ */
@@ -695,7 +786,8 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 	    CH == 2 ? xa_pack_state(p0[CH - 1], p1[CH - 1]) : 0u);
 }
 
-/* K1 for one stream: wave w of the grid takes chunks 64w .. 64w+63 */
+/* K1 for one stream: wave w of the grid takes chunks 64w .. 64w+63 and
+ * settles their boundaries */
 template <int BITS, int CH>
 __global__ __launch_bounds__(XA_SPEC_CPW, 8 / XA_SPEC_WPB) void
 xa_decode_spec(xa_dec_args a)
@@ -708,18 +800,16 @@ xa_decode_spec(xa_dec_args a)
 	__shared__ __attribute__((aligned(16))) uint8_t
 	    lds[XA_SPEC_WPB * L::REGION];
 	const uint32_t wchunk0 = blockIdx.x * XA_SPEC_CPW + wv * 64u;
-	const uint32_t q = wchunk0 + lane;
 	uint2 gs, ex;
 	spec_wave2<BITS, CH>(a, lds + wv * L::REGION, wchunk0, a.pace, gs, ex);
-	list_mismatches(a, lane, q, true, gs, ex);
-	if (q < a.nchunks) {
-		a.g[q] = gs;
-		a.e[q] = ex;
-	}
+#ifdef XA_DBG_LINE_RUNS
+	return;		/* diagnostic build: its PCM is garbage */
+#endif
+	settle_wave<BITS, CH>(a, lane, wchunk0, gs, ex);
 }
 
 /* ------------------------------------------------------------------ */
-/* K2: boundaries between K1 workgroups, and the sequential tail        */
+/* K2: the sequential tail                                              */
 
 /* binary min-heap over queue[0..n) (single thread) */
 __device__ static void
@@ -758,19 +848,23 @@ heap_pop(uint32_t *h, uint32_t &n)
 }
 
 /*
- * The sequential tail (lane 0 of one wave): drain the re-check queue in chunk
- * order (a heap, so even a pathological cascade costs O(n log n)
- * bookkeeping), then publish the status words and reset the control words.
- * Queue entries are >= 1, so 0 ends the loop.
+ * The sequential tail (thread 0): drain the re-check queue in chunk order
+ * (a heap, so even a pathological cascade costs O(n log n) bookkeeping),
+ * then publish the status words and reset the control words.  Entries
+ * outside [1, nchunks) -- stale ones, from a workspace a failed launch left
+ * behind -- are skipped, so nothing is read out of range.
  */
-template <int BITS, int CH, bool BUF>
+template <int BITS, int CH>
 __device__ __forceinline__ void
 drain_tail(const xa_dec_args &a)
 {
-	const uint32_t nq = a.ctl[XA_CTL_NQ];
+	const uint32_t nq = min(*a.nq, a.qcap), nc = a.nchunks;
 	uint32_t n = 0, tail = 0;
-	for (uint32_t i = 0; i < nq; i++)
-		heap_push(a.queue, n, a.queue[i]);
+	for (uint32_t i = 0; i < nq; i++) {
+		const uint32_t q = a.queue[i];
+		if (q >= 1u && q < nc)
+			heap_push(a.queue, n, q);
+	}
 	while (n > 0) {
 		const uint32_t q = heap_pop(a.queue, n);
 		const uint2 s = a.e[q - 1], gq = a.g[q];
@@ -778,171 +872,97 @@ drain_tail(const xa_dec_args &a)
 			continue;
 		tail++;
 		uint2 ex;
-		const bool met = fix_chunk<BITS, CH, BUF>(a, q, s, ex);
+		const bool met = fix_chunk<BITS, CH>(a, q, s, ex, (int64_t)q * a.C);
 		a.g[q] = s;
-		if (!met && q + 1 < a.nchunks)
-			heap_push(a.queue, n, q + 1);
+		if (!met) {
+			a.e[q] = ex;
+			if (q + 1 < nc)
+				heap_push(a.queue, n, q + 1);
+		}
 	}
-	const uint2 fin = a.e[a.nchunks - 1];
+	const uint2 fin = a.e[nc - 1];
 	a.status[XA_ST_ERR] = a.ctl[XA_CTL_ERR];
 	a.status[XA_ST_STATE_L] = fin.x;
 	a.status[XA_ST_STATE_R] = fin.y;
 	a.status[XA_ST_FIXED] = a.ctl[XA_CTL_FIXED];
 	a.status[XA_ST_TAIL] = tail;
-	a.status[XA_ST_CHUNKS] = a.nchunks;
+	a.status[XA_ST_CHUNKS] = nc;
 	a.status[XA_ST_C] = a.C;
 	a.status[XA_ST_W] = a.W;
 	a.ctl[XA_CTL_ERR] = 0xffffffffu;
 	a.ctl[XA_CTL_NQ] = 0;
 	a.ctl[XA_CTL_FIXED] = 0;
-	a.ctl[XA_CTL_TICKET] = 0;
-	a.ctl[XA_CTL_NL] = 0;
+	a.ctl[XA_CTL_OVF] = 0;
 }
 
 /*
- * Arrival ticket of K2 (MI355X_MICROARCH.md inter-workgroup recipe): every
- * wave's stores done at the barrier, then lane 0's agent release and its
- * wait, then the ticket -- the release only in workgroups that stored.
- * Returns (on every thread) whether this is the last workgroup; that one
- * then acquires.  A one-workgroup grid is its own last.
+ * After a queue overflow (XA_CTL_OVF) the queue is rebuilt from scratch:
+ * every boundary of [first, end) (global chunk indices) whose entry state
+ * differs from its predecessor's exit, found by the whole workgroup, written
+ * as queue entries; skip(Q) drops indices that are no boundary (a batch
+ * stream's chunk 0, padding).  Returns on every thread; thread 0 then holds
+ * the new length in *nq.
  */
-__device__ __forceinline__ bool
-k2_last(uint32_t *ticket, bool wrote)
+template <typename F>
+__device__ __forceinline__ void
+rebuild_queue(const uint2 *e, const uint2 *g, uint32_t *queue, uint32_t *nq,
+    uint32_t first, uint32_t end, F &&skip)
 {
-	__shared__ uint32_t last;
-	if (gridDim.x == 1) {
-		__syncthreads();
-		return true;
-	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	const int any = __syncthreads_or(wrote);
-	if (threadIdx.x == 0) {
-		if (any) {
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		}
-		last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+	__shared__ uint32_t cnt;
+	if (threadIdx.x == 0)
+		cnt = 0;
+	__syncthreads();
+	for (uint32_t Q = first + threadIdx.x; Q < end; Q += blockDim.x) {
+		if (skip(Q))
+			continue;
+		const uint2 s = e[Q - 1], gq = g[Q];
+		if (s.x != gq.x || s.y != gq.y)
+			queue[atomicAdd(&cnt, 1u)] = Q;
 	}
 	__syncthreads();
-	if (!last)
-		return false;
-	/* acquire: this CU now sees every other workgroup's writes */
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	return true;
+	if (threadIdx.x == 0)
+		*nq = cnt;
+	__syncthreads();
 }
 
 /*
- * The chunks K2 checks, entry i of `nb + nl`: the first chunk of every wave
- * but the first (i < nb: chunk 64 (i + 1)), then the chunks K1 listed.
+ * K2 for one stream: one workgroup.  Everything K1 could not settle itself
+ * is in the queue (cascades out of a chunk, boundaries whose record did not
+ * come in time); thread 0 re-checks it in chunk order and publishes the
+ * status.  Its cost is a launch and, almost always, an empty queue.
  */
-__device__ __forceinline__ uint32_t
-k2_entry(const uint32_t *list, uint32_t nb, uint32_t i)
+template <int BITS, int CH>
+__global__ __launch_bounds__(XA_TAIL_THREADS) void
+xa_decode_tail(xa_dec_args a)
 {
-	return i < nb ? 64u * (i + 1u) : list[i - nb];
-}
-
-/*
- * This thread's first entry of K2's grid-stride loop.  Entries are dealt
- * round-robin over the workgroups first, then over the waves of each, then
- * over the lanes: the listed mismatches are contiguous, and given to
- * consecutive lanes they would pile dozens of serial repairs onto a few
- * waves of a few CUs (a repaired block costs ~1 us on a lone lane but ~4 us
- * with four busy waves on one CU, DESIGN.md §5 round 2 exp. 11).
- */
-__device__ __forceinline__ uint32_t
-k2_first()
-{
-	constexpr uint32_t WPB = XA_FIX_THREADS / 64;
-	return ((threadIdx.x & 63u) * WPB + (threadIdx.x >> 6)) * gridDim.x +
-	    blockIdx.x;
-}
-
-/*
- * K2 for one stream.  Each thread takes entries of the check list in a
- * grid-stride loop: chunk q is compared with its predecessor's exit and
- * repaired on a mismatch; a repair that does not meet the stored
- * trajectory queues q+1 for the tail.  Entries are the boundaries K1 could
- * not check (a wave's first chunk against the previous wave's last) and
- * the inner-wave mismatches K1 listed, so K2's work grows with the
- * mismatches, not with the stream.  The last workgroup then drains the
- * queue in chunk order and publishes the status.
- */
-template <int BITS, int CH, bool BUF>
-__global__ __launch_bounds__(XA_FIX_THREADS) void
-xa_decode_fix(xa_dec_args a)
-{
-#ifdef XA_DBG_K2_EMPTY
-	return;		/* diagnostic build: the kernel boundary alone */
-#endif
-	const uint32_t n = a.nchunks;
-	const uint64_t *e64 = (const uint64_t *)a.e;
-	const uint64_t *g64 = (const uint64_t *)a.g;
-	const uint32_t nb = (n + 63u) / 64u - 1u;
-	const uint32_t total = nb + min(*a.nlist, a.lcap);
-	bool wrote = false;
-	uint32_t nfix = 0;
-	for (uint32_t i = k2_first(); i < total; i += gridDim.x * XA_FIX_THREADS) {
-		const uint32_t q = k2_entry(a.list, nb, i);
-		/* e[q-1] may be rewritten concurrently by chunk q-1's fixer;
-		 * whichever value is read is recorded in g[q], and that fixer
-		 * queues q for the tail, which re-checks it */
-		const uint64_t ev = __hip_atomic_load(&e64[q - 1], __ATOMIC_RELAXED,
-		    __HIP_MEMORY_SCOPE_AGENT);
-		const uint64_t gv = g64[q];
-		if (q >= n || ev == gv)
-			continue;
-		const uint2 s = make_uint2((uint32_t)ev, (uint32_t)(ev >> 32));
-		uint2 ex;
-		const bool met = fix_chunk<BITS, CH, BUF>(a, q, s, ex);
-		wrote = true;
-		nfix++;
-		a.g[q] = s;
-		if (!met && q + 1 < n) {
-			uint32_t j = atomicAdd(&a.ctl[XA_CTL_NQ], 1u);
-			a.queue[j] = q + 1;
-		}
-	}
-	if (nfix)
-		atomicAdd(&a.ctl[XA_CTL_FIXED], nfix);
-#ifdef XA_DBG_K2_NOTICKET
-	/* diagnostic build: workgroup 0 drains without waiting for the others */
-	(void)wrote;
-	if (blockIdx.x != 0 || threadIdx.x != 0)
-		return;
-#else
-	if (!k2_last(&a.ctl[XA_CTL_TICKET], wrote) || threadIdx.x != 0)
-		return;
-#endif
-	drain_tail<BITS, CH, BUF>(a);
-}
-
-/* K2's grid: enough threads for every wave boundary plus a list of up to
- * half the chunks in one pass, at most XA_FIX_MAXWG workgroups -- about one
- * per CU, so that dense repairs (mix W: a quarter of the chunks) spread
- * over the whole chip; a longer list takes more passes of the grid-stride
- * loop */
-#ifndef XA_FIX_MAXWG
-#define XA_FIX_MAXWG 256u
-#endif
-static unsigned
-k2_grid(uint64_t nwaves, uint64_t nchunks)
-{
-	const uint64_t want = nwaves - 1 + nchunks / 2;
-	uint64_t g = (want + XA_FIX_THREADS - 1) / XA_FIX_THREADS;
-	if (g < 1)
-		g = 1;
-	return (unsigned)(g < XA_FIX_MAXWG ? g : XA_FIX_MAXWG);
+	if (*a.ovf != 0u)
+		rebuild_queue(a.e, a.g, a.queue, a.nq, 1u, a.nchunks,
+		    [](uint32_t) { return false; });
+	if (threadIdx.x == 0)
+		drain_tail<BITS, CH>(a);
 }
 
 /* ------------------------------------------------------------------ */
 
+/* the record tag of a launch: process-wide, never 0 */
+static uint32_t
+next_tag(void)
+{
+	static uint32_t t;
+	uint32_t v;
+	do
+		v = __atomic_add_fetch(&t, 1u, __ATOMIC_RELAXED);
+	while (v == 0u);
+	return v;
+}
+
 template <int BITS, int CH>
 static hipError_t
-launch(const xa_dec_args &a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
+launch(const xa_dec_args &a0, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
 {
+	xa_dec_args a = a0;
+	a.tag = next_tag();
 	const unsigned grid = (a.nchunks + XA_SPEC_CPW - 1) / XA_SPEC_CPW;
-	const unsigned grid2 = k2_grid((a.nchunks + 63u) / 64u, a.nchunks);
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
 	hipLaunchKernelGGL((xa_decode_spec<BITS, CH>), dim3(grid),
@@ -952,13 +972,8 @@ launch(const xa_dec_args &a, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
 #ifdef XA_DBG_LINE_RUNS
 	return hipGetLastError();	/* its PCM is garbage: nothing to verify */
 #endif
-	/* buffer-descriptor windows need 32-bit byte offsets */
-	if ((uint64_t)a.eblocks * geo<BITS, CH>::EBSZ < (1ull << 32) - 256u)
-		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, true>), dim3(grid2),
-		    dim3(XA_FIX_THREADS), 0, st, a);
-	else
-		hipLaunchKernelGGL((xa_decode_fix<BITS, CH, false>), dim3(grid2),
-		    dim3(XA_FIX_THREADS), 0, st, a);
+	hipLaunchKernelGGL((xa_decode_tail<BITS, CH>), dim3(1),
+	    dim3(XA_TAIL_THREADS), 0, st, a);
 	return hipGetLastError();
 }
 
@@ -1031,10 +1046,14 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.g = b.g + d.cbase;
 	a.e = b.e + d.cbase;
 	a.queue = b.queue;
-	a.list = b.list;
-	a.lcap = 64u * b.nwaves;
-	a.nlist = &b.ctl[XA_CTL_NL];
-	a.lbase = d.cbase;
+	a.nq = &b.ctl[XA_CTL_NQ];
+	a.qcap = 2u * 64u * b.nwaves;
+	a.qbase = d.cbase;
+	a.ovf = &b.ctl[XA_CTL_OVF];
+	a.exits = b.exits + d.cbase / 64u;
+	a.tag = b.tag;
+	a.spin = b.spin;
+	a.flags = b.flags;
 	a.ctl = b.sctl + sid * XA_SCTL_WORDS;	/* ERR and FIXED line up */
 	a.status = b.status + sid * XA_ST_WORDS;
 	return a;
@@ -1057,8 +1076,10 @@ struct batch_lds {
 
 /*
  * K1 over a batch: wave w decodes 64 chunks of stream wstream[w] with that
- * stream's format (wave-uniform dispatch, no divergence), then lists its
- * inner mismatches as in xa_decode_spec (global chunk indices).
+ * stream's format (wave-uniform dispatch, no divergence), then settles
+ * their boundaries as xa_decode_spec does (the wave before it belongs to
+ * the same stream unless this wave starts the stream; queue entries are
+ * global chunk indices).
  */
 __global__ __launch_bounds__(XA_SPEC_CPW, 8 / XA_SPEC_WPB) void
 xa_decode_spec_batch(xa_batch_args b)
@@ -1090,54 +1111,64 @@ xa_decode_spec_batch(xa_batch_args b)
 	const uint32_t fmt = __builtin_amdgcn_readfirstlane(b.streams[sid].fmt);
 	const uint32_t wchunk0 = 64u * w -
 	    __builtin_amdgcn_readfirstlane(b.streams[sid].cbase);
-	const uint32_t q = wchunk0 + lane;
 	uint8_t *region = lds + wv * batch_lds::REGION;
 	with_format(fmt, [&](auto bc, auto cc) {
 		constexpr int BITS = decltype(bc)::value, CH = decltype(cc)::value;
 		uint2 gs, ex;
 		spec_wave2<BITS, CH>(a, region, wchunk0, lockstep ? b.pace : 0u,
 		    gs, ex);
-		list_mismatches(a, lane, q, true, gs, ex);
-		if (q < a.nchunks) {
-			a.g[q] = gs;
-			a.e[q] = ex;
-		}
+		settle_wave<BITS, CH>(a, lane, wchunk0, gs, ex);
 	});
 }
 
-/* fix_chunk in a stream's format (a per-lane switch: no generic lambda, so
- * the argument block stays in registers) */
+/* fix_chunk in a stream's format, for the one-thread tail (windows based at
+ * the chunk itself) */
 __device__ __forceinline__ bool
 fix_any(const xa_dec_args &a, uint32_t fmt, uint32_t q, uint2 s, uint2 &ex)
 {
+	const int64_t bb = (int64_t)q * a.C;
 	switch (fmt) {
 	case 8 | 2 << 8:
-		return fix_chunk<8, 2>(a, q, s, ex);
+		return fix_chunk<8, 2>(a, q, s, ex, bb);
 	case 6 | 2 << 8:
-		return fix_chunk<6, 2>(a, q, s, ex);
+		return fix_chunk<6, 2>(a, q, s, ex, bb);
 	case 4 | 2 << 8:
-		return fix_chunk<4, 2>(a, q, s, ex);
+		return fix_chunk<4, 2>(a, q, s, ex, bb);
 	case 8 | 1 << 8:
-		return fix_chunk<8, 1>(a, q, s, ex);
+		return fix_chunk<8, 1>(a, q, s, ex, bb);
 	case 6 | 1 << 8:
-		return fix_chunk<6, 1>(a, q, s, ex);
+		return fix_chunk<6, 1>(a, q, s, ex, bb);
 	default:
-		return fix_chunk<4, 1>(a, q, s, ex);
+		return fix_chunk<4, 1>(a, q, s, ex, bb);
 	}
 }
 
+/* global chunk Q is no boundary of its stream (the stream's chunk 0, or a
+ * padding slot of its last wave) */
+__device__ __forceinline__ bool
+batch_no_boundary(const xa_batch_args &b, uint32_t Q)
+{
+	const xa_batch_stream &d = b.streams[b.wstream[Q / 64]];
+	const uint32_t q = Q - d.cbase;
+	return q == 0 || q >= d.nchunks;
+}
+
 /*
- * Sequential tail of a batch (lane 0 of one wave): drain the re-check queue
- * in global chunk order.  Global chunk
- * indices never cross streams (a stream's chunk 0 is never queued).
+ * Sequential tail of a batch (thread 0): drain the re-check queue in global
+ * chunk order.  Global chunk indices never cross streams (a stream's chunk
+ * 0 is never queued); entries that are no boundary (stale ones) are
+ * skipped.
  */
 __device__ __forceinline__ void
 drain_batch(const xa_batch_args &b)
 {
-	const uint32_t nq = b.ctl[XA_CTL_NQ];
+	const uint32_t nc = 64u * b.nwaves, nq = min(b.ctl[XA_CTL_NQ], 2u * nc);
 	uint32_t n = 0;
-	for (uint32_t i = 0; i < nq; i++)
-		heap_push(b.queue, n, b.queue[i]);
+	for (uint32_t i = 0; i < nq; i++) {
+		const uint32_t Q = b.queue[i];
+		if (Q >= 1u && Q < nc && !batch_no_boundary(b, Q))
+			heap_push(b.queue, n, Q);
+	}
 	while (n > 0) {
 		const uint32_t Q = heap_pop(b.queue, n);
 		const uint2 s = b.e[Q - 1], gq = b.g[Q];
@@ -1150,51 +1181,27 @@ drain_batch(const xa_batch_args &b)
 		const bool met = fix_any(a, b.streams[sid].fmt, q, s, ex);
 		b.g[Q] = s;
 		b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_TAIL]++;
-		if (!met && q + 1 < a.nchunks)
-			heap_push(b.queue, n, Q + 1);
+		if (!met) {
+			b.e[Q] = ex;
+			if (q + 1 < a.nchunks)
+				heap_push(b.queue, n, Q + 1);
+		}
 	}
 }
 
 /*
- * K2 over a batch: the same grid-stride check and repair as xa_decode_fix
- * over global chunk indices.  A wave's first chunk is checked only where it
- * continues the previous wave's stream (stream-local index not 0, and not
- * a padding slot past the stream's last chunk); listed chunks always are.
- * Repairs run in the chunk's stream format.  The last workgroup drains the
- * cascades and publishes every stream's status.
+ * K2 over a batch: one workgroup drains what the batch K1 queued, in global
+ * chunk order, repairing in each chunk's stream format, then publishes every
+ * stream's status.
  */
-__global__ __launch_bounds__(XA_FIX_THREADS) void
-xa_decode_fix_batch(xa_batch_args b)
+__global__ __launch_bounds__(XA_TAIL_THREADS) void
+xa_decode_tail_batch(xa_batch_args b)
 {
-	const uint64_t *e64 = (const uint64_t *)b.e;
-	const uint64_t *g64 = (const uint64_t *)b.g;
-	const uint32_t nb = b.nwaves - 1u;
-	const uint32_t total = nb + min(b.ctl[XA_CTL_NL], 64u * b.nwaves);
-	bool wrote = false;
-	for (uint32_t i = k2_first(); i < total; i += gridDim.x * XA_FIX_THREADS) {
-		const uint32_t Q = k2_entry(b.list, nb, i);
-		const uint32_t sid = b.wstream[Q / 64];
-		const xa_batch_stream &d = b.streams[sid];
-		const uint32_t q = Q - d.cbase, nch = d.nchunks, fmt = d.fmt;
-		const uint64_t ev = __hip_atomic_load(&e64[Q - 1], __ATOMIC_RELAXED,
-		    __HIP_MEMORY_SCOPE_AGENT);
-		const uint64_t gv = g64[Q];
-		if (q == 0 || q >= nch || ev == gv)
-			continue;
-		const xa_dec_args a = batch_stream_args(b, sid);
-		const uint2 s = make_uint2((uint32_t)ev, (uint32_t)(ev >> 32));
-		uint2 ex;
-		const bool met = fix_any(a, fmt, q, s, ex);
-		wrote = true;
-		b.g[Q] = s;
-		atomicAdd(&b.sctl[sid * XA_SCTL_WORDS + XA_SCTL_FIXED], 1u);
-		if (!met && q + 1 < nch) {
-			uint32_t j = atomicAdd(&b.ctl[XA_CTL_NQ], 1u);
-			b.queue[j] = Q + 1;
-		}
-	}
-	if (!k2_last(&b.ctl[XA_CTL_TICKET], wrote))
-		return;
+	if (b.ctl[XA_CTL_OVF] != 0u)
+		rebuild_queue(b.e, b.g, b.queue, &b.ctl[XA_CTL_NQ], 1u,
+		    64u * b.nwaves, [&](uint32_t Q) {
+			    return batch_no_boundary(b, Q);
+		    });
 	if (threadIdx.x == 0)
 		drain_batch(b);
 	__syncthreads();
@@ -1202,12 +1209,12 @@ xa_decode_fix_batch(xa_batch_args b)
 	 * in full before any is written, so the dependent loads (descriptor,
 	 * then the last chunk's exit state) overlap across streams */
 	constexpr int XA_PUB = 4;
-	for (uint32_t s0 = 0; s0 < b.nstreams; s0 += XA_FIX_THREADS * XA_PUB) {
+	for (uint32_t s0 = 0; s0 < b.nstreams; s0 += XA_TAIL_THREADS * XA_PUB) {
 		uint32_t err[XA_PUB], fix[XA_PUB], tail[XA_PUB], nch[XA_PUB], cc[XA_PUB];
 		uint2 fin[XA_PUB];
 #pragma unroll
 		for (int j = 0; j < XA_PUB; j++) {
-			const uint32_t s = min(s0 + threadIdx.x + XA_FIX_THREADS * j,
+			const uint32_t s = min(s0 + threadIdx.x + XA_TAIL_THREADS * j,
 			    b.nstreams - 1);
 			const xa_batch_stream &dd = b.streams[s];
 			const uint32_t *sc = b.sctl + s * XA_SCTL_WORDS;
@@ -1220,7 +1227,7 @@ xa_decode_fix_batch(xa_batch_args b)
 		}
 #pragma unroll
 		for (int j = 0; j < XA_PUB; j++) {
-			const uint32_t s = s0 + threadIdx.x + XA_FIX_THREADS * j;
+			const uint32_t s = s0 + threadIdx.x + XA_TAIL_THREADS * j;
 			if (s >= b.nstreams)
 				continue;
 			uint32_t *sc = b.sctl + s * XA_SCTL_WORDS;
@@ -1240,24 +1247,24 @@ xa_decode_fix_batch(xa_batch_args b)
 	}
 	if (threadIdx.x == 0) {
 		b.ctl[XA_CTL_NQ] = 0;
-		b.ctl[XA_CTL_TICKET] = 0;
-		b.ctl[XA_CTL_NL] = 0;
+		b.ctl[XA_CTL_OVF] = 0;
 	}
 }
 
 hipError_t
-xa_decode_batch_launch(const xa_batch_args &b, hipStream_t st, hipEvent_t ev0,
+xa_decode_batch_launch(const xa_batch_args &b0, hipStream_t st, hipEvent_t ev0,
     hipEvent_t ev1)
 {
+	xa_batch_args b = b0;
+	b.tag = next_tag();
 	const unsigned grid = (b.nwaves + XA_SPEC_WPB - 1) / XA_SPEC_WPB;
-	const unsigned grid2 = k2_grid(b.nwaves, 64ull * b.nwaves);
 	if (ev0 != NULL)
 		(void)hipEventRecord(ev0, st);
 	hipLaunchKernelGGL(xa_decode_spec_batch, dim3(grid), dim3(XA_SPEC_CPW), 0,
 	    st, b);
 	if (ev1 != NULL)
 		(void)hipEventRecord(ev1, st);
-	hipLaunchKernelGGL(xa_decode_fix_batch, dim3(grid2), dim3(XA_FIX_THREADS),
+	hipLaunchKernelGGL(xa_decode_tail_batch, dim3(1), dim3(XA_TAIL_THREADS),
 	    0, st, b);
 	return hipGetLastError();
 }

@@ -79,6 +79,20 @@ struct plan {
 	uint32_t	nchunks;
 };
 
+/*
+ * Longest chunk: the decode kernel repairs a wave's chunks through one
+ * buffer descriptor based at the wave's first eblock, so a wave's 64 chunks
+ * of XA (33 B per 8-bit channel block, the largest) must stay under 4 GiB.
+ * Only a manual chunk length or a giant batch stream ever gets near it.
+ */
+static uint32_t
+max_chunk(unsigned ch)
+{
+	const uint32_t G = XA_CHUNK_Q(ch);
+	return (uint32_t)((((1ull << 32) - (1ull << 20)) / (64ull * 33u * ch)) /
+	    G * G);
+}
+
 /* chunk plan for one stream: automatic (above), or tune->chunk eblocks */
 static void
 plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
@@ -97,6 +111,8 @@ plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
 			c = MIN_CHUNK;
 	}
 	p->C = round_up(c, G);
+	if (p->C > max_chunk(ch))
+		p->C = max_chunk(ch);
 	p->nchunks = (uint32_t)(((uint64_t)eblocks + p->C - 1) / p->C);
 }
 
@@ -125,11 +141,32 @@ pick_pace(uint32_t ns, bool batch, const bjxa_hip_tuning_t *t)
 	return ns <= (batch ? PACE_MAX_NS_BATCH : PACE_MAX_NS) ? 1u : 0u;
 }
 
+/* workspace layout: control words, g[n], e[n], the queue (2n entries: a
+ * chunk may be queued twice, as a late boundary and after a cascade), then
+ * one 16-B exit record per wave */
+/* the verify pass's test knobs (tuning variant bits 18, 19) */
+#define XA_VARIANT_NORECORD	0x40000u
+#define XA_VARIANT_NOWAIT	0x80000u
+
+static void
+verify_knobs(const bjxa_hip_tuning_t *t, uint32_t *spin, uint32_t *flags)
+{
+	const uint32_t v = t ? t->variant : 0u;
+	*spin = (v & XA_VARIANT_NOWAIT) ? 0u : XA_SPIN_TICKS;
+	*flags = (v & XA_VARIANT_NORECORD) ? XA_F_NORECORD : 0u;
+}
+
+static size_t
+ws_exits_off(uint32_t nchunks)
+{
+	return (XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 8) + 15) &
+	    ~(size_t)15;
+}
+
 static size_t
 ws_bytes(uint32_t nchunks)
 {
-	/* g, e, queue (2x: the tail heap may hold duplicates), K1's list */
-	return XA_CTL_WORDS * 4 + (size_t)nchunks * (8 + 8 + 8 + 4) + 64;
+	return ws_exits_off(nchunks) + (size_t)(nchunks + 63) / 64 * 16 + 64;
 }
 
 extern "C" size_t
@@ -159,6 +196,12 @@ bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream)
 	}
 	if (!bjxa__gpu_present()) {
 		errno = ENODEV;
+		return -1;
+	}
+	/* all of it: no exit record of an earlier user of the memory survives
+	 * (records of this process's earlier launches carry other tags) */
+	if (hipMemsetAsync(d_ws, 0, ws_len, (hipStream_t)stream) != hipSuccess) {
+		errno = EIO;
 		return -1;
 	}
 	hipLaunchKernelGGL(xa_ws_init, dim3(1), dim3(64), 0,
@@ -212,16 +255,23 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.g = (uint2 *)(ws + XA_CTL_WORDS * 4);
 	a.e = a.g + p.nchunks;
 	a.queue = (uint32_t *)(a.e + p.nchunks);
-	a.list = a.queue + 2 * (size_t)p.nchunks;
-	a.nlist = &a.ctl[XA_CTL_NL];
-	a.lcap = p.nchunks;
-	a.lbase = 0;
+	a.nq = &a.ctl[XA_CTL_NQ];
+	a.qcap = 2u * p.nchunks;
+	a.qbase = 0;
+	a.ovf = &a.ctl[XA_CTL_OVF];
+	a.exits = (uint4 *)(ws + ws_exits_off(p.nchunks));
+	a.tag = 0;	/* set per launch */
+	verify_knobs(tune, &a.spin, &a.flags);
 	a.status = d_status;
 	hipEvent_t e0 = tune ? (hipEvent_t)tune->ev_spec[0] : NULL;
 	hipEvent_t e1 = tune ? (hipEvent_t)tune->ev_spec[1] : NULL;
 	const hipError_t rc = xa_decode_launch(a, s->bits, s->channels,
 	    (hipStream_t)stream, e0, e1);
 	if (rc != hipSuccess) {
+		/* the first kernel may have run without the tail that resets
+		 * the control words: leave the workspace initialised again */
+		(void)hipGetLastError();
+		(void)bjxa_hip_workspace_init(d_ws, ws_len, stream);
 		errno = EIO;
 		return -1;
 	}
@@ -421,6 +471,11 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		if (k == 0)
 			k = 1;
 		uint64_t c = (E + 64 * k - 1) / (64 * k);
+		if (c > max_chunk(ch)) {
+			/* more waves, so that a wave's XA stays under 4 GiB */
+			k = (E + 64ull * max_chunk(ch) - 1) / (64ull * max_chunk(ch));
+			c = (E + 64 * k - 1) / (64 * k);
+		}
 		if (c < MIN_CHUNK)
 			c = MIN_CHUNK;
 		c = (c + G - 1) / G * G;
@@ -466,8 +521,8 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	const size_t o_g = o_wav + al64(nwaves * 4);
 	const size_t o_e = o_g + nc * 8;
 	const size_t o_q = o_e + nc * 8;
-	const size_t o_l = o_q + 2 * nc * 4;
-	const size_t len = o_l + nc * 4;
+	const size_t o_x = al64(o_q + 2 * nc * 4);	/* exit records */
+	const size_t len = o_x + nwaves * 16;
 	uint8_t *ws = NULL;
 	if (ws_cache != NULL && *ws_cap >= len) {
 		ws = (uint8_t *)*ws_cache;
@@ -515,7 +570,9 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	a.g = (uint2 *)(ws + o_g);
 	a.e = (uint2 *)(ws + o_e);
 	a.queue = (uint32_t *)(ws + o_q);
-	a.list = (uint32_t *)(ws + o_l);
+	a.exits = (uint4 *)(ws + o_x);
+	a.tag = 0;	/* set per launch */
+	verify_knobs(tune, &a.spin, &a.flags);
 	a.ctl = (uint32_t *)ws;
 	a.sctl = (uint32_t *)(ws + o_sctl);
 	a.status = NULL;
@@ -528,6 +585,9 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	    hipStreamSynchronize((hipStream_t)stream) != hipSuccess;
 	free(hs);
 	free(hw);
+	if (!bad)
+		bad = hipMemsetAsync(ws + o_x, 0, nwaves * 16, (hipStream_t)stream) !=
+		    hipSuccess;
 	if (!bad) {
 		hipLaunchKernelGGL(xa_batch_init, dim3((n + 255) / 256), dim3(256),
 		    0, (hipStream_t)stream, a.ctl, a.sctl, n);
@@ -555,8 +615,18 @@ bjxa_hip_batch_decode_async(bjxa_hip_batch_t *b, uint32_t *d_status,
 	b->args.status = d_status;
 	if (xa_decode_batch_launch(b->args, (hipStream_t)stream,
 	    tune ? (hipEvent_t)tune->ev_spec[0] : NULL,
-	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess ||
-	    hipEventRecord(b->done, (hipStream_t)stream) != hipSuccess) {
+	    tune ? (hipEvent_t)tune->ev_spec[1] : NULL) != hipSuccess) {
+		/* the first kernel may have run without the tail that resets
+		 * the control words: reset them for the next decode */
+		(void)hipGetLastError();
+		hipLaunchKernelGGL(xa_batch_init, dim3((b->args.nstreams + 255) /
+		    256), dim3(256), 0, (hipStream_t)stream, b->args.ctl,
+		    b->args.sctl, b->args.nstreams);
+		(void)hipGetLastError();
+		errno = EIO;
+		return -1;
+	}
+	if (hipEventRecord(b->done, (hipStream_t)stream) != hipSuccess) {
 		errno = EIO;
 		return -1;
 	}
@@ -595,6 +665,8 @@ struct bjxa__gpu {
 	uint8_t		*h_small;	/* pinned: small-call in | out | status */
 	uint8_t		*d_small;	/* its device view */
 	uint32_t	*d_status;
+	bool		ws_stale;	/* a call failed: initialise the
+					 * workspace again before the next */
 };
 
 static int
@@ -753,7 +825,7 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 	const size_t out_full = (size_t)eblocks * 64u * ch;
 	bjxa_hip_stream_t s;
 	uint32_t st[BJXA_HIP_STATUS_WORDS];
-	int fresh = g->d_ws == NULL;
+	int fresh = g->d_ws == NULL || g->ws_stale;
 
 	size_t wsn = bjxa_hip_decode_workspace(eblocks, ch, NULL);
 	if (grow(&g->d_in, &g->in_cap, in_bytes + 16) < 0 ||
@@ -766,6 +838,8 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 	}
 	if (fresh && bjxa_hip_workspace_init(g->d_ws, g->ws_cap, g->stream) < 0)
 		return -1;
+	/* cleared once the status of this call has come back */
+	g->ws_stale = true;
 	if (hipMemcpyAsync(g->d_in, src, in_bytes, hipMemcpyHostToDevice,
 	    g->stream) != hipSuccess)
 		return io_fail();
@@ -783,6 +857,7 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 	    g->stream) != hipSuccess || hipStreamSynchronize(g->stream) !=
 	    hipSuccess)
 		return io_fail();
+	g->ws_stale = false;
 	*err_cb = st[XA_ST_ERR];
 	if (st[XA_ST_ERR] != 0xffffffffu) {
 		/* stop before the failing eblock, as the reference does; the

@@ -50,9 +50,14 @@ typedef struct {
 					 * batches: bit 16 forces, bit 17
 					 * forbids the longer chunks planned
 					 * for packed PCM images (automatic:
-					 * by layout); other bits reserved
-					 * (0).  Pass the same tuning to
-					 * bjxa_hip_decode_workspace. */
+					 * by layout); test knobs of the
+					 * verify pass: bit 18 makes every
+					 * wave leave its first boundary to
+					 * the sequential tail, bit 19 stops
+					 * waves waiting for the exit record
+					 * of the wave before them; other
+					 * bits reserved (0).  Pass the same
+					 * tuning to bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 
 /*
@@ -61,13 +66,16 @@ typedef struct {
  *      nibble is >= 5, 0xffffffff if none (the reference's EPROTO, :550)
  *  [1] exit state L (prev[0] | prev[1] << 16)
  *  [2] exit state R
- *  [3] chunks repaired by the verify pass, [4] by the sequential tail,
+ *  [3] chunks repaired inside the decode kernel, [4] by the sequential
+ *      tail (cascades, and boundaries the decode kernel left to it),
  *  [5] chunks, [6] chunk length and [7] warm-up length used (eblocks)
  */
 #define BJXA_HIP_STATUS_WORDS 8
 
-/* workspace bytes for one stream of `eblocks`; zero it once (or call
- * bjxa_hip_workspace_init) before first use; it is left reusable */
+/* workspace bytes for one stream of `eblocks`; call bjxa_hip_workspace_init
+ * once before first use; a completed decode leaves it reusable.  A decode
+ * whose launch fails re-initialises it itself; after a device fault (an
+ * error from the stream) initialise it again before reusing it */
 size_t bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
     const bjxa_hip_tuning_t *tune);
 int bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream);

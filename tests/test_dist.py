@@ -237,6 +237,22 @@ def test_bench_world_mismatch():
     assert rc == 2 and line is None and "WORLD_SIZE=1" in err
 
 
+def test_bench_stuck_rank_times_out():
+    """A rank that stops answering (BJXA_BENCH_STALL_RANK: rank 1 sleeps
+    before its first collective) fails the job within the process group's
+    timeout (BJXA_BENCH_PG_TIMEOUT, 180 s by default), with the rank that
+    gave up named, instead of waiting torch's default 10 minutes."""
+    import time
+    t = time.time()
+    rc, line, err = _bench(["--gpus", "2", "--streams", "4", "--eblocks", "100",
+                            "--steps", "1", "--warmup", "0"],
+                           {"BJXA_BENCH_PG_TIMEOUT": "5", "BJXA_BENCH_STALL_RANK": "1",
+                            "BJXA_BENCH_STALL_S": "90"}, timeout=200)
+    assert rc != 0 and line is None
+    assert time.time() - t < 80
+    assert "bench.py rank 0:" in err
+
+
 def test_bench_force_pg_one_rank():
     """`--gpus 1 --force-pg` starts one rank under torch.distributed.run and
     joins a process group at world size 1, so the control plane's

@@ -34,8 +34,9 @@ def test_worst_case_mix_full_size(built):
 @pytest.mark.parametrize("bits,ch", [(8, 2), (8, 1), (4, 2), (6, 1)])
 def test_auto_plan_short_warmup(built, bits, ch):
     """The automatic plan on a ragged stream with a cut last block and a
-    2-eblock warm-up, so many chunks need repair: inside K1 workgroups
-    (verified and repaired by K1 itself) and at their boundaries (K2)."""
+    2-eblock warm-up, so many chunks need repair: each wave of the decode
+    kernel repairs its own chunks, inside the wave and at the boundary with
+    the wave before it (its exit record)."""
     eb = 2_500_003
     frames = eb * 32 - 7
     xa = synth.stream(eb, bits, ch, "A", seed=5)

@@ -1,0 +1,121 @@
+"""The verify/repair pass inside the decode kernel (xa_decode.hip
+settle_wave) and what it leaves to the sequential tail: cascades, wave
+boundaries whose exit record does not come (forced with the tuning knobs
+VARIANT_NORECORD / VARIANT_NOWAIT), and a workspace left inconsistent by a
+failed launch -- every case bit-exact against the
+oracle, which restates src/libbjxa.c:533-578 / :602-661."""
+import numpy as np
+import pytest
+
+import bjxa_amd
+import oracle
+from bjxa_amd import synth
+from gpu_util import dev_decode, require_gpu, status_state
+from test_gpu_batch import FORMATS, check, make, run_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("bits,ch", [(8, 2), (6, 1), (4, 2)])
+def test_long_cascades(built, bits, ch):
+    """Mix W (gain 4 only, ranges 12-15: the slowest resync), no warm-up,
+    16-eblock chunks: nearly every chunk is repaired in the decode kernel
+    and repairs that never meet the stored trajectory cascade through the
+    tail, across waves."""
+    eb = 400_003
+    frames = eb * 32 - 3
+    xa = synth.stream(eb, bits, ch, "W", seed=11)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, (7, -7, 70, -70), frames)
+    got, st = dev_decode(xa, eb, bits, ch, frames=frames, state=(7, -7, 70, -70),
+                         chunk=16, warmup=0, want_status=True)
+    assert np.array_equal(got, ref)
+    assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
+    assert st[3] > st[5] // 4          # repairs in the decode kernel
+    assert st[4] > 0                   # and cascades in the tail
+
+
+@pytest.mark.parametrize("variant", [bjxa_amd.VARIANT_NORECORD, bjxa_amd.VARIANT_NOWAIT,
+                                     bjxa_amd.VARIANT_NORECORD | bjxa_amd.VARIANT_NOWAIT])
+@pytest.mark.parametrize("mix", ["A", "W"])
+def test_boundaries_left_to_tail(built, variant, mix):
+    """Waves that get no exit record from the wave before them (none
+    written, or none waited for) queue their first boundary for the tail,
+    which re-checks and repairs it in chunk order."""
+    eb = 1_000_000
+    xa = synth.stream(eb, 8, 2, mix, seed=12)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, 8, 2)
+    got, st = dev_decode(xa, eb, 8, 2, want_status=True, variant=variant, warmup=0)
+    assert np.array_equal(got, ref)
+    assert status_state(st) == st_ref
+    if variant & bjxa_amd.VARIANT_NORECORD:
+        assert st[4] > 0
+
+
+def _layout(nchunks):
+    """Byte offsets of the single-stream workspace (xa_gpu.hip ws_bytes):
+    control words, g, e, queue (2n), exit records (16-B aligned)."""
+    g = 256
+    e = g + 8 * nchunks
+    q = e + 8 * nchunks
+    x = (q + 8 * nchunks + 15) // 16 * 16
+    return g, e, q, x
+
+
+@pytest.mark.parametrize("poke", ["full", "stale"])
+def test_stale_workspace(built, poke):
+    """A workspace as a failed launch could leave it: the queue length at
+    (full) or below (stale) capacity with garbage entries, some out of
+    range, and garbage exit records.  The next decode on it must still be
+    bit-exact -- past the capacity the tail re-checks every boundary, and
+    entries outside the stream are skipped -- and leave it clean."""
+    torch = require_gpu()
+    eb, bits, ch = 600_000, 8, 2
+    xa = synth.stream(eb, bits, ch, "W", seed=13)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch)
+    src = torch.from_numpy(xa).cuda()
+    dst = torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
+    ws_len = bjxa_amd.decode_workspace_size(eb, ch, 0, 0)
+    ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    bjxa_amd.workspace_init(ws.data_ptr(), ws_len, sh)
+
+    def decode():
+        dst.fill_(0x5A)
+        bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, bits, ch,
+                               ws.data_ptr(), ws_len, status.data_ptr(), (0, 0, 0, 0), 0, 0,
+                               sh)
+        torch.cuda.synchronize()
+        return dst.cpu().numpy().view(np.int16), status.cpu().numpy().view(np.uint32).copy()
+
+    got, st = decode()
+    assert np.array_equal(got, ref)
+    n = int(st[5])
+    g, e, q, x = _layout(n)
+    assert x + 16 * ((n + 63) // 64) <= ws_len
+    rng = np.random.default_rng(14)
+    ctl = ws[:256].view(torch.int32)
+    ctl[1] = 2 * n if poke == "full" else n // 3          # XA_CTL_NQ
+    junk = rng.integers(0, 1 << 32, 2 * n, dtype=np.uint64).astype(np.uint32)
+    junk[::7] = rng.integers(1, n, junk[::7].size)        # some in range
+    ws[q:q + 8 * n].copy_(torch.from_numpy(junk.view(np.uint8)))
+    nx = 16 * ((n + 63) // 64)
+    ws[x:x + nx].copy_(torch.from_numpy(rng.integers(0, 256, nx, dtype=np.uint8)))
+    got, st = decode()
+    assert np.array_equal(got, ref)
+    assert status_state(st) == st_ref
+    assert int(ctl[1].item()) == 0 and int(ctl[3].item()) == 0   # NQ, OVF reset
+    got, st = decode()                                             # and reusable
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("variant", [bjxa_amd.VARIANT_NORECORD, bjxa_amd.VARIANT_NOWAIT])
+def test_batch_boundaries_left_to_tail(built, variant):
+    """The batch kernel with the same knobs: every format, cascades."""
+    specs = [make(40000 + 777 * i, bits, ch, 600 + i, mix="W" if i % 2 else "A",
+                  cut=i % 3)
+             for i, (bits, ch) in enumerate(FORMATS * 2)]
+    pcms, st = run_batch(specs, chunk=16, warmup=0, variant=variant)
+    check(specs, pcms, st)
+    if variant & bjxa_amd.VARIANT_NORECORD:
+        assert st[:, 4].sum() > 0
