@@ -11,10 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <algorithm>
 #include <mutex>
-#include <utility>
-#include <vector>
 
 #include "xa_decode.h"
 #include "xa_gpu.h"
@@ -352,32 +349,74 @@ stream_ok(const bjxa_hip_stream_t *s)
 /*
  * Streams whose PCM images are carved out of one large device allocation
  * (as bjxa_hip_decode_files does, or a caller packing a batch into one
- * buffer) lie in one physically contiguous run, and there a chunk length
- * whose PCM lane stride is a multiple of 8 KiB lines every lane of every
- * stream up on the same HBM channels: C5's per-GPU share at 8 GPUs (64
- * eblocks = 8 KiB) runs 0.43 ms packed against 0.30 ms in allocations of
- * their own, whatever the VA gaps between the streams (DESIGN.md §5 round 2
- * exp. 14, R3-7).  Such streams get chunks one quantum longer.  Streams in
- * allocations of their own do not pay the penalty (even where a caching
- * allocator puts two in one segment), and there the longer chunks would
- * only cost time (round 2 exp. 16), so the planner asks the runtime which
- * allocation each PCM image belongs to and lengthens the chunks of streams
- * that share one with at least XA_PACKED_MIN others.  Tuning variant bit 16
- * forces the longer chunks for every stream, bit 17 forbids them.
+ * buffer) decode slower when their chunk length puts the lanes' PCM 8 KiB
+ * apart: C5's per-GPU share at 8 GPUs (64 eblocks = 8 KiB) runs 0.43 ms
+ * packed against 0.30 ms in allocations of their own, whatever the VA gaps
+ * between the streams (DESIGN.md §5 round 2 exp. 14, R3-7, R4-11).  Why is
+ * not settled: one hypothesis is that one physically contiguous run puts
+ * every lane of every stream on the same HBM channels, but a store-only
+ * probe pays the 8 KiB stride in both layouts.  Such
+ * streams get chunks one quantum longer.  Streams in allocations of their
+ * own do not pay the penalty, and there the longer chunks only cost time
+ * (round 2 exp. 16), so the planner asks the runtime which allocation each
+ * PCM image belongs to and lengthens the chunks of streams that share an
+ * allocation of at least XA_PACKED_SPAN bytes with at least XA_PACKED_MIN - 1
+ * others.  The span keeps out a caching allocator's shared segments: torch
+ * carves mid-size tensors out of 20 MiB segments, and 512 streams of 2 MiB
+ * PCM so placed (ten to a segment) run 0.3187 ms at 64-eblock chunks
+ * against 0.3477 at 68; an 8 KiB lane stride only
+ * arises for batches of ~1 GiB of PCM on 256 CUs, so an allocation that
+ * holds eight such images and reaches 64 MiB is the caller's own.  Tuning
+ * variant bit 16 forces the longer chunks for every stream, bit 17 forbids
+ * them.
  */
 #define XA_VARIANT_DECOR	0x10000u
 #define XA_VARIANT_NODECOR	0x20000u
 #define XA_PACKED_MIN		8u
+#define XA_PACKED_SPAN		(64ull << 20)
 
-static void
-packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t,
-    std::vector<uint8_t> &packed)
+struct pcm_base {
+	uintptr_t	base;	/* the allocation holding the PCM image */
+	uint32_t	idx;
+};
+
+static int
+by_base(const void *x, const void *y)
+{
+	const struct pcm_base *a = (const struct pcm_base *)x;
+	const struct pcm_base *b = (const struct pcm_base *)y;
+	if (a->base != b->base)
+		return a->base < b->base ? -1 : 1;
+	return a->idx < b->idx ? -1 : (a->idx > b->idx);
+}
+
+/*
+ * packed[i] = 1 for the streams whose PCM shares an allocation of at least
+ * XA_PACKED_SPAN bytes with at least XA_PACKED_MIN - 1 others (or all / none
+ * under the tuning bits).
+ * Returns a calloc'ed array of n flags, or NULL with errno ENOMEM.  The
+ * runtime's error state is cleared after an address it cannot place (that
+ * error is not the caller's).
+ */
+static uint8_t *
+packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t)
 {
 	const uint32_t v = t ? t->variant : 0u;
-	packed.assign(n, (v & XA_VARIANT_DECOR) ? 1 : 0);
+	uint8_t *packed = (uint8_t *)calloc(n, 1);
+	if (packed == NULL) {
+		errno = ENOMEM;
+		return NULL;
+	}
+	if (v & XA_VARIANT_DECOR)
+		memset(packed, 1, n);
 	if (v & (XA_VARIANT_DECOR | XA_VARIANT_NODECOR) || n < XA_PACKED_MIN)
-		return;
-	std::vector<std::pair<uintptr_t, uint32_t>> base(n);
+		return packed;
+	struct pcm_base *base = (struct pcm_base *)calloc(n, sizeof *base);
+	if (base == NULL) {
+		free(packed);
+		errno = ENOMEM;
+		return NULL;
+	}
 	bool failed = false;
 	for (uint32_t i = 0; i < n; i++) {
 		hipDeviceptr_t b = NULL;
@@ -386,21 +425,26 @@ packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t,
 		    hipSuccess) {
 			b = NULL;	/* not a device allocation we can see */
 			failed = true;
+		} else if (sz < XA_PACKED_SPAN) {
+			b = NULL;	/* a small allocation: never "packed" */
 		}
-		base[i] = { (uintptr_t)b, i };
+		base[i].base = (uintptr_t)b;
+		base[i].idx = i;
 	}
 	if (failed)
-		(void)hipGetLastError();	/* not the caller's error */
-	std::sort(base.begin(), base.end());
+		(void)hipGetLastError();
+	qsort(base, n, sizeof *base, by_base);
 	for (uint32_t i = 0; i < n;) {
 		uint32_t j = i;
-		while (j < n && base[j].first == base[i].first)
+		while (j < n && base[j].base == base[i].base)
 			j++;
-		if (base[i].first != 0 && j - i >= XA_PACKED_MIN)
+		if (base[i].base != 0 && j - i >= XA_PACKED_MIN)
 			for (uint32_t k = i; k < j; k++)
-				packed[base[k].second] = 1;
+				packed[base[k].idx] = 1;
 		i = j;
 	}
+	free(base);
+	return packed;
 }
 
 /*
@@ -456,10 +500,12 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	    DEFAULT_WARMUP;
 	const uint32_t W = (w + 7) & ~7u;	/* a whole chunk quantum of every format */
 
-	std::vector<uint8_t> packed;
-	packed_pcm(s, n, tune, packed);
+	uint8_t *packed = packed_pcm(s, n, tune);
+	if (packed == NULL)
+		return NULL;
 	xa_batch_stream *hs = (xa_batch_stream *)calloc(n, sizeof *hs);
 	if (hs == NULL) {
+		free(packed);
 		errno = ENOMEM;
 		return NULL;
 	}
@@ -496,6 +542,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		hs[i].fmt = s[i].bits | ch << 8;
 		nwaves += (nch + 63) / 64;
 	}
+	free(packed);
 	if (64 * nwaves > 0x7fffffffu) {
 		free(hs);
 		errno = EINVAL;

@@ -186,42 +186,92 @@ def test_batch_streams_share_k1_workgroups(built):
     assert st[:, 3].sum() > 0
 
 
-def run_packed(specs, chunk, packed, variant=0):
-    """run_batch with every stream's XA and PCM carved from one allocation
-    each, back to back (packed), or in allocations of their own."""
+class RawBuffers:
+    """Device buffers each from a hipMalloc of its own (outside torch's
+    caching allocator, which carves mid-size tensors out of shared
+    segments), as uint8 tensors; freed on exit."""
+
+    def __init__(self):
+        import ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        self.hip.hipFree.argtypes = [ctypes.c_void_p]
+        self.ptrs = []
+
+    def get(self, n, fill=0x5A):
+        import ctypes
+        torch = require_gpu()
+        p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(p), n) == 0
+        self.ptrs.append(p.value)
+
+        class Iface:
+            __cuda_array_interface__ = {"shape": (n,), "typestr": "|u1",
+                                        "data": (p.value, False), "version": 2}
+        t = torch.as_tensor(Iface(), device="cuda")
+        t.fill_(fill)
+        return t
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        require_gpu().cuda.synchronize()
+        for p in self.ptrs:
+            self.hip.hipFree(p)
+
+
+PACKED_SPAN = 64 << 20      # xa_gpu.hip XA_PACKED_SPAN
+
+
+def run_packed(specs, chunk, layout, variant=0):
+    """run_batch with the PCM images laid out as `layout`:
+      "packed"  back to back at the start of one allocation of at least
+                PACKED_SPAN bytes (a caller's own big buffer)
+      "raw"     a hipMalloc of its own each
+      "torch"   a torch tensor each (small ones share the caching
+                allocator's segments)"""
     torch = require_gpu()
     sizes = [eb * 64 * ch for _, eb, _, ch, _, _ in specs]
-    if packed:
-        big = torch.full((sum(sizes),), 0x5A, dtype=torch.uint8, device="cuda")
-        offs = np.cumsum([0] + sizes[:-1])
-        dsts = [big[o:o + n] for o, n in zip(offs, sizes)]
-    else:
-        dsts = [torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda") for n in sizes]
-    srcs = [torch.from_numpy(np.ascontiguousarray(xa)).cuda() for xa, *_ in specs]
-    streams = [{"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb, "bits": bits,
-                "channels": ch, "frames": frames, "state": state}
-               for s, d, (xa, eb, bits, ch, frames, state) in zip(srcs, dsts, specs)]
-    status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
-    sh = torch.cuda.current_stream().cuda_stream
-    with bjxa_amd.Batch(streams, chunk, -1, sh, variant) as b:
-        b.decode(status.data_ptr(), sh)
-        torch.cuda.synchronize()
-    out = [d.cpu().numpy().view(np.int16)[:frames * ch].copy()
-           for d, (_, _, _, ch, frames, _) in zip(dsts, specs)]
+    with RawBuffers() as raw:
+        if layout == "packed":
+            big = torch.full((max(sum(sizes), PACKED_SPAN),), 0x5A, dtype=torch.uint8,
+                             device="cuda")
+            offs = np.cumsum([0] + sizes[:-1])
+            dsts = [big[o:o + n] for o, n in zip(offs, sizes)]
+        elif layout == "raw":
+            dsts = [raw.get(n) for n in sizes]
+        else:
+            dsts = [torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda") for n in sizes]
+        srcs = [torch.from_numpy(np.ascontiguousarray(xa)).cuda() for xa, *_ in specs]
+        streams = [{"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
+                    "bits": bits, "channels": ch, "frames": frames, "state": state}
+                   for s, d, (xa, eb, bits, ch, frames, state) in zip(srcs, dsts, specs)]
+        status = torch.zeros(len(specs) * bjxa_amd.STATUS_WORDS, dtype=torch.int32,
+                             device="cuda")
+        sh = torch.cuda.current_stream().cuda_stream
+        with bjxa_amd.Batch(streams, chunk, -1, sh, variant) as b:
+            b.decode(status.data_ptr(), sh)
+            torch.cuda.synchronize()
+        out = [d.cpu().numpy().view(np.int16)[:frames * ch].copy()
+               for d, (_, _, _, ch, frames, _) in zip(dsts, specs)]
     return out, status.cpu().numpy().view(np.uint32).reshape(len(specs), -1).copy()
 
 
-@pytest.mark.parametrize("packed", [False, True])
-def test_batch_packed_layout_plan(built, packed):
+@pytest.mark.parametrize("layout", ["raw", "torch", "packed"])
+def test_batch_packed_layout_plan(built, layout):
     """Streams whose PCM lane stride is a multiple of 8 KiB (here 64 stereo
-    eblocks per lane) get chunks one quantum longer when their PCM images
-    are packed back to back in one allocation, and keep them otherwise;
-    bit-exact either way, including with the choice forced off and on."""
+    eblocks per lane) get chunks one quantum longer only when eight or more
+    PCM images share one allocation of at least 64 MiB (a caller's packed
+    buffer); in allocations of their own, and in torch tensors that share
+    the caching allocator's (smaller) segments, they keep them (DESIGN.md §5
+    R4-7, R5-4).  Bit-exact either way, including with the choice forced off
+    and on."""
     specs = [make(4096, 8, 2, 900 + i, cut=(5 if i == 3 else 0)) for i in range(8)]
-    pcms, st = run_packed(specs, 128, packed)
+    pcms, st = run_packed(specs, 128, layout)
     check(specs, pcms, st)
-    assert (st[:, 6] == (68 if packed else 64)).all()
+    assert (st[:, 6] == (68 if layout == "packed" else 64)).all()
     for v, c in ((bjxa_amd.VARIANT_NODECOR, 64), (bjxa_amd.VARIANT_DECOR, 68)):
-        pcms, st = run_packed(specs, 128, packed, v)
+        pcms, st = run_packed(specs, 128, layout, v)
         check(specs, pcms, st)
         assert (st[:, 6] == c).all()

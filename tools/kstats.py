@@ -1,6 +1,6 @@
 """Median / mean / count of each decode kernel's duration in a rocprofv3
-kernel-trace CSV, and for spec -> fix pairs the gap between them and the
-span from the spec kernel's start to the fix kernel's end:
+kernel-trace CSV, and for spec -> fix (round 5: tail) pairs the gap between
+them and the span from the spec kernel's start to the fix kernel's end:
 python3 tools/kstats.py <run_kernel_trace.csv> [label]"""
 import collections
 import csv
@@ -16,7 +16,7 @@ def main(path, label=""):
             if "xa_" in n:
                 s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
                 d[n.split("(")[0]].append((e - s) / 1e3)
-                seq.append((s, e, "spec" in n, "fix" in n))
+                seq.append((s, e, "spec" in n, "fix" in n or "tail" in n))
     for n, v in sorted(d.items()):
         v.sort()
         print("%-12s %-40s n=%4d median %8.2f us  mean %8.2f us  min %8.2f" % (

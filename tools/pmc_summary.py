@@ -39,7 +39,7 @@ def rows(pattern):
 def short(name):
     """Kernel key: name plus <bits,ch> for the templated kernels, so the
     C3 (8-bit stereo) and C2 (8-bit mono) launches of one run stay apart."""
-    for k in ("xa_decode_spec", "xa_decode_fix", "xa_decode_region", "xa_encode_waves",
+    for k in ("xa_decode_spec", "xa_decode_tail", "xa_decode_fix", "xa_encode_waves",
               "xa_ws_init"):
         if k in name:
             i = name.find(k + "<")
