@@ -67,6 +67,25 @@ static_assert(XA_SCTL_FIXED == XA_CTL_FIXED && XA_SCTL_ERR == XA_CTL_ERR,
 #define XA_LB 128
 #define XA_NST 16	/* store instructions per group (G * OB / 16) */
 
+/*
+ * Where lane j's XA_LB-byte line sits in the wave's output stage.  Lanes
+ * write their lines a 16-B piece at a time, all lanes the same piece
+ * (ds_write_b128: 16 lanes a pass, each on 4 of the 64 banks), and the
+ * stores read them back 8 lanes per line, lines j and j+1 in one pass.
+ * Lines 128 B apart plus 16 B per line pair (XA_OST_SKEW) keep both
+ * conflict-free: the 16 writers' offsets 32j + 4(j/2) dwords are distinct
+ * mod 64 in steps of 4, and lines 2m and 2m+1 start 32 dwords apart.  The
+ * round-4 pitch of 144 B is conflict-free for the writes only.
+ */
+#ifndef XA_OST_SKEW
+#define XA_OST_SKEW 1
+#endif
+__host__ __device__ constexpr int
+ost_line(int j)
+{
+	return XA_OST_SKEW ? j * XA_LB + (j >> 1) * 16 : j * (XA_LB + 16);
+}
+
 /* one 16-B piece of PCM, streamed out: non-temporal (the line stays in the
  * XCD's L2 until evicted), or with XA_PCM_SC1 system-coherent write-through
  * (MI355X_MICROARCH.md: sc1 stores leave L2 at once and drop the line) */
@@ -96,13 +115,14 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
     uint32_t wchunk0, uint64_t wstart_b, uint32_t chunk_bytes, uint32_t rel_off,
     bool wave_full, bool clean, uint8_t *gbase, const uint8_t *lbase)
 {
-	constexpr int LINE = XA_LB + 16, P = XA_LB / 16, LPI = 64 / P;
+	constexpr int P = XA_LB / 16, LPI = 64 / P, LSTEP = ost_line(LPI);
+	static_assert(ost_line(LPI + 1) - ost_line(1) == LSTEP, "stage stride");
 	if (wave_full) {
 		uint8_t *gp = gbase + rel_off;
 		const uint64_t istride = (uint64_t)LPI * chunk_bytes;
 #pragma unroll
 		for (int i = 0; i < P; i++) {
-			const u32x4a v = *(const u32x4a *)(lbase + i * LPI * LINE);
+			const u32x4a v = *(const u32x4a *)(lbase + i * LSTEP);
 			pcm_store(gp + i * istride, v);
 		}
 		return;
@@ -116,7 +136,7 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 		const uint64_t istride = (uint64_t)LPI * chunk_bytes;
 #pragma unroll
 		for (int i = 0; i < P; i++) {
-			const u32x4a v = *(const u32x4a *)(lbase + i * LPI * LINE);
+			const u32x4a v = *(const u32x4a *)(lbase + i * LSTEP);
 			uint8_t *q = gp + i * istride;
 			if (q + 16 <= end)
 				pcm_store(q, v);
@@ -137,7 +157,7 @@ store_lines(const xa_dec_args &a, const uint8_t *obuf, int lane,
 		const uint64_t off = wsb + (uint64_t)j * cb + ro + (uint64_t)pc * 16u;
 		if (cj >= nch)
 			continue;
-		const uint8_t *from = obuf + j * LINE + pc * 16;
+		const uint8_t *from = obuf + ost_line(j) + pc * 16;
 		/* (off < lim first, so that no bound can wrap) */
 		if (off >= lim)
 			continue;
@@ -163,8 +183,7 @@ template <int BITS, int CH> struct geo2 {
 
 /* one wave's LDS: the half-wave landing buffer, then the output stage */
 template <int BITS, int CH> struct spec_lds2 {
-	static constexpr int LINE = XA_LB + 16;
-	static constexpr int REGION = geo2<BITS, CH>::HALF + 64 * LINE;
+	static constexpr int REGION = geo2<BITS, CH>::HALF + ost_line(64);
 	static_assert(REGION >= 64 * 8, "the exit exchange needs 8 B per lane");
 };
 
@@ -550,7 +569,7 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 	typedef geo<BITS, CH> g;
 	typedef geo2<BITS, CH> g2;
 	constexpr int G = g::G, OB = g::OB, EBSZ = g::EBSZ, GDW = g::GDW;
-	constexpr int RD = g2::RD, LB = XA_LB, LINE = LB + 16;
+	constexpr int RD = g2::RD, LB = XA_LB;
 	static_assert(G * OB / 16 == XA_NST, "store count per group");
 
 	const int lane = threadIdx.x & 63;
@@ -592,8 +611,8 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 	constexpr int P = LB / 16;
 	uint8_t *gbase = a.dst + wstart_b + (uint64_t)(lane / P) * chunk_bytes +
 	    (lane % P) * 16;
-	const uint8_t *lbase = ost + (lane / P) * LINE + (lane % P) * 16;
-	uint8_t *line = ost + lane * LINE;
+	const uint8_t *lbase = ost + ost_line(lane / P) + (lane % P) * 16;
+	uint8_t *line = ost + ost_line(lane);
 	const uint64_t full_blocks = a.pcm_bytes / OB;
 	const bool wave_full = wchunk0 + 63u < a.nchunks &&
 	    (uint64_t)(wstart + 64 * (int64_t)Cw) <= full_blocks;
