@@ -428,15 +428,23 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     evs.close()
     torch.cuda.synchronize(dev)
     st = slots[0]["status"].cpu().numpy().view(np.uint32).copy()
+    # every slot's PCM and the status words the API defines (first error,
+    # exit state, plan) equal slot 0's; the repair counters (words 3, 4)
+    # may differ: whether a wave's boundary is repaired inside K1 or by the
+    # tail depends on timing when other kernels share the GPU
+    st0 = slots[0]["status"].cpu().numpy().view(np.uint32)
     same = all(torch.equal(sl["dst"], slots[0]["dst"]) and
-               torch.equal(sl["status"], slots[0]["status"]) for sl in slots[1:])
+               all(int(a) == int(b) for i, (a, b) in enumerate(zip(
+                   sl["status"].cpu().numpy().view(np.uint32), st0)) if i not in (3, 4))
+               for sl in slots[1:])
 
-    ok, cpu = None, None
+    ok, cpu, exact = None, None, None
     if verify or cpu_leg:
         import oracle
         out = slots[0]["dst"].cpu().numpy().view(np.int16)
         ref, _, _, _ = oracle.decode(xa_np, eb, bits, ch)   # also the discarded pass
-        ok = bool(np.array_equal(out, ref)) and same
+        exact = bool(np.array_equal(out, ref))
+        ok = exact and same
         del out
         if cpu_leg:
             times = []
@@ -463,7 +471,8 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
             "elapsed": elapsed, "serial": serial, "pipeline": depth, "pipeline_cal": cal,
             "step_ms": spread(step_ms, depth), "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
-            "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "cpu": cpu}
+            "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "pcm_equal_oracle": exact,
+            "slots_agree": same, "cpu": cpu}
 
 
 def product_cpu_core(xa_np, eb, bits, ch, sample_eb=1_000_000):
@@ -911,7 +920,9 @@ def other_stream_line(o, steps, world=1):
             "step_ms": o["step_ms"],
             "spec_ms": round(o["spec_ms"], 4), "spec_samples": o["spec_samples"],
             "frac": round(o["alg_bytes"] / (o["spec_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "chunk": int(o["status"][6]), "bit_exact": o["ok"], "cpu_baseline": o["cpu"]}
+            "chunk": int(o["status"][6]), "bit_exact": o["ok"],
+            "pcm_equal_oracle": o["pcm_equal_oracle"], "slots_agree": o["slots_agree"],
+            "cpu_baseline": o["cpu"]}
 
 
 def main_stream(args, workload, dev, world, rank, others=None):

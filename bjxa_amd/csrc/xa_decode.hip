@@ -945,6 +945,58 @@ rebuild_queue(const uint2 *e, const uint2 *g, uint32_t *queue, uint32_t *nq,
 }
 
 /*
+ * Before the one-thread drain: the whole workgroup drops the queued entries
+ * that need no repair (keep(Q) false: out of range, no boundary, or entry
+ * state already equal to the predecessor's exit), so the drain's serial
+ * loop only sees real mismatches.  Dropping an entry whose states match is
+ * safe: if a repair earlier in the drain changes that predecessor's exit,
+ * the cascade queues the entry again.  Up to XA_TAIL_KEEP survivors are
+ * compacted to the front of the queue; past that the queue is left whole
+ * and the drain checks every entry itself.  This keeps the tail cheap when
+ * many waves left their first boundary to it (their records came late:
+ * other kernels holding the GPU).
+ */
+#define XA_TAIL_KEEP 4096
+
+template <typename F>
+__device__ __forceinline__ void
+filter_queue(uint32_t *queue, uint32_t *nq, uint32_t qcap, F &&keep)
+{
+	__shared__ uint32_t cnt;
+	__shared__ uint32_t kept[XA_TAIL_KEEP];
+	if (threadIdx.x == 0)
+		cnt = 0;
+	__syncthreads();
+	const uint32_t n = min(*nq, qcap);
+	for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+		const uint32_t Q = queue[i];
+		if (keep(Q)) {
+			const uint32_t j = atomicAdd(&cnt, 1u);
+			if (j < XA_TAIL_KEEP)
+				kept[j] = Q;
+		}
+	}
+	__syncthreads();
+	const uint32_t c = cnt;
+	if (c <= XA_TAIL_KEEP) {
+		for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
+			queue[i] = kept[i];
+		__syncthreads();
+		if (threadIdx.x == 0)
+			*nq = c;
+	}
+	__syncthreads();
+}
+
+/* the entry state of chunk Q differs from its predecessor's exit */
+__device__ __forceinline__ bool
+differs(const uint2 *e, const uint2 *g, uint32_t Q)
+{
+	const uint2 s = e[Q - 1], gq = g[Q];
+	return s.x != gq.x || s.y != gq.y;
+}
+
+/*
  * K2 for one stream: one workgroup.  Everything K1 could not settle itself
  * is in the queue (cascades out of a chunk, boundaries whose record did not
  * come in time); thread 0 re-checks it in chunk order and publishes the
@@ -957,6 +1009,10 @@ xa_decode_tail(xa_dec_args a)
 	if (*a.ovf != 0u)
 		rebuild_queue(a.e, a.g, a.queue, a.nq, 1u, a.nchunks,
 		    [](uint32_t) { return false; });
+	else
+		filter_queue(a.queue, a.nq, a.qcap, [&](uint32_t q) {
+			return q >= 1u && q < a.nchunks && differs(a.e, a.g, q);
+		});
 	if (threadIdx.x == 0)
 		drain_tail<BITS, CH>(a);
 }
@@ -1220,6 +1276,12 @@ xa_decode_tail_batch(xa_batch_args b)
 		rebuild_queue(b.e, b.g, b.queue, &b.ctl[XA_CTL_NQ], 1u,
 		    64u * b.nwaves, [&](uint32_t Q) {
 			    return batch_no_boundary(b, Q);
+		    });
+	else
+		filter_queue(b.queue, &b.ctl[XA_CTL_NQ], 2u * 64u * b.nwaves,
+		    [&](uint32_t Q) {
+			    return Q >= 1u && Q < 64u * b.nwaves &&
+				!batch_no_boundary(b, Q) && differs(b.e, b.g, Q);
 		    });
 	if (threadIdx.x == 0)
 		drain_batch(b);

@@ -68,6 +68,7 @@ def test_bench_c5_two_ranks_shared_gpu(built):
     assert cp["checksums_match_oracle"] is True and line["bit_exact"] is True
     c3 = line["other_configs"]["C3_weak"]
     assert c3["bit_exact"] is True and c3["value"] > 0
+    assert c3["pcm_equal_oracle"] is True and c3["slots_agree"] is True
 
 
 def test_bench_c5_three_ranks_shared_gpu(built):
@@ -102,10 +103,13 @@ def test_bench_default_line_c3(built):
     cfg = line["config"]
     assert cfg["pipeline"] in (1, 2) and line["ms_per_step_serial"] > 0
     cal = cfg["pipeline_cal"]
-    assert set(cal) == {"depth1_ms", "depth2_ms"}
-    # two in flight only when they beat one at a time by the margin
-    two = cal["depth2_ms"] < cal["depth1_ms"] * (1 - 0.01) - 1e-4
-    one = cal["depth2_ms"] > cal["depth1_ms"] * (1 - 0.01) + 1e-4
+    assert set(cal) == {"depth1_ms", "depth2_ms", "runs_ms"}
+    # two in flight only when every run of them beats every run one at a
+    # time by the margin
+    runs = cal["runs_ms"]
+    assert len(runs["depth1"]) == len(runs["depth2"]) >= 3
+    two = max(runs["depth2"]) < min(runs["depth1"]) * (1 - 0.01) - 1e-4
+    one = max(runs["depth2"]) > min(runs["depth1"]) * (1 - 0.01) + 1e-4
     assert (cfg["pipeline"] == 2) if two else (cfg["pipeline"] == 1) if one else True
 
 
