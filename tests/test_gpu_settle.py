@@ -119,3 +119,20 @@ def test_batch_boundaries_left_to_tail(built, variant):
     check(specs, pcms, st)
     if variant & bjxa_amd.VARIANT_NORECORD:
         assert st[:, 4].sum() > 0
+
+
+def test_manual_chunk_capped(built):
+    """A manual chunk length whose wave would span more than 4 GiB of XA
+    (64 chunks of 2,000,000 8-bit stereo eblocks) is capped by the planner
+    (xa_gpu.hip max_chunk), so the repair windows' 32-bit descriptor
+    offsets stay in range; the decode is still bit-exact.  Warm-up 0 makes
+    the second chunk's entry wrong, so its repair runs through the
+    descriptor."""
+    eb = 2_100_000
+    xa = synth.stream(eb, 8, 2, "W", seed=15)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, 8, 2)
+    got, st = dev_decode(xa, eb, 8, 2, chunk=2_000_000, warmup=0, want_status=True)
+    assert np.array_equal(got, ref)
+    assert status_state(st) == st_ref
+    cap = ((1 << 32) - (1 << 20)) // (64 * 33 * 2) // 4 * 4
+    assert st[6] == cap and st[5] == -(-eb // cap)
