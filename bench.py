@@ -397,7 +397,8 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     samples = eb * 32 * ch
     xa_np = synth.stream(eb, bits, ch, args.mix, seed=rank)
     src = torch.from_numpy(xa_np).to(dev)
-    ws_len = bjxa_amd.decode_workspace_size(eb, ch, args.chunk, args.warm_blocks)
+    ws_len = bjxa_amd.decode_workspace_size(eb, ch, args.chunk, args.warm_blocks,
+                                            args.variant)
     slots = pipeline_slots(args.pipeline or 2, dev, lambda k: {
         "src": src if k == 0 else src.clone(),
         "dst": torch.empty(eb * 64 * ch, dtype=torch.uint8, device=dev),
@@ -411,7 +412,8 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
         sl = slots[i % len(slots)]
         bjxa_amd.decode_device(sl["src"].data_ptr(), sl["dst"].data_ptr(), eb, eb * 32, bits, ch,
                                sl["ws"].data_ptr(), ws_len, sl["status"].data_ptr(),
-                               (0, 0, 0, 0), args.chunk, args.warm_blocks, sl["sh"], ev)
+                               (0, 0, 0, 0), args.chunk, args.warm_blocks, sl["sh"], ev,
+                               args.variant)
 
     for i in range(args.warmup):
         step(i)
@@ -581,7 +583,7 @@ def cpu_batch_baseline(name, inputs):
 
 
 def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, eblocks=0,
-              cpu_leg=False, bad_stream=-1, pipeline=1):
+              cpu_leg=False, bad_stream=-1, pipeline=1, variant=0):
     """Decode (this rank's share of) a batch config with bjxa_hip_batch_* --
     all streams per launch -- `steps` times after `warmup` untimed steps,
     then time EV_SAMPLES more launches with events.  Returns this rank's
@@ -619,7 +621,8 @@ def run_batch(name, steps, warmup, dev, verify, nstreams=0, rank=0, world=1, ebl
                 desc = [{"d_src": s.data_ptr(), "d_dst": d.data_ptr(), "eblocks": eb,
                          "bits": bits, "channels": ch}
                         for s, d, (_, bits, ch, eb, _) in zip(sl["srcs"], sl["dsts"], inputs)]
-                sl["batch"] = stack.enter_context(bjxa_amd.Batch(desc, stream=sl["sh"]))
+                sl["batch"] = stack.enter_context(bjxa_amd.Batch(desc, stream=sl["sh"],
+                                                                 variant=variant))
             torch.cuda.synchronize(dev)
 
             def step(i, ev=(None, None)):
@@ -792,6 +795,8 @@ def parse_args(argv=None):
     ap.add_argument("--mix", default="A", choices=["A", "F", "W", "Z"])
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--warm-blocks", type=int, default=-1)
+    ap.add_argument("--variant", type=lambda v: int(v, 0), default=0,
+                    help="tuning variant bits of every decode (include/bjxa_hip.h)")
     ap.add_argument("--streams", type=int, default=0, help="C5 streams (default 1024)")
     ap.add_argument("--eblocks", type=int, default=0, help="C5 eblocks per stream (65,536)")
     ap.add_argument("--bad-stream", type=int, default=-1,
@@ -844,6 +849,7 @@ def only_other(args):
         o = other_stream_line(run_workload(name, args, dev, 1, 0, verify, cpu_leg), args.steps)
     elif name in BATCHES:
         o = run_batch(name, args.steps, args.warmup, dev, verify, cpu_leg=cpu_leg,
+                      variant=args.variant,
                       pipeline=args.pipeline)
         for k in ("checksums", "ref_checksums", "shard"):
             o.pop(k)

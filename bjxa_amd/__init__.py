@@ -289,6 +289,7 @@ def encode_wav(data, bits=6):
 VARIANT_PACE_OFF = 15 << 8   # tuning variant bits 8-11: no pacing barriers
 VARIANT_NORECORD = 0x40000   # test knob: every wave boundary goes to the sequential tail
 VARIANT_NOWAIT = 0x80000     # test knob: waves do not wait for the previous wave's record
+VARIANT_PIPE2 = 0x100000     # plan for two decodes in flight (one K1 workgroup per CU)
 VARIANT_DECOR = 0x10000      # batches: the longer chunks of packed PCM images, forced
 VARIANT_NODECOR = 0x20000    # batches: the same, never
 

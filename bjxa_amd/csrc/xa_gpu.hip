@@ -65,6 +65,22 @@ target_lanes(void)
 	return c * 2u * 256u;
 }
 
+/*
+ * Tuning variant bit 20: the caller keeps two decodes in flight (two HIP
+ * streams, a workspace each).  Plan for one K1 workgroup per CU instead of
+ * two: chunks twice as long, so half the warm-up per decoded eblock, and
+ * the two launches in flight fill the CUs between them.  Alone such a
+ * launch runs at half occupancy.
+ */
+#define XA_VARIANT_PIPE2	0x100000u
+
+static uint32_t
+plan_lanes(const bjxa_hip_tuning_t *t)
+{
+	const uint32_t lanes = target_lanes();
+	return (t && (t->variant & XA_VARIANT_PIPE2)) ? lanes / 2u : lanes;
+}
+
 static uint32_t
 round_up(uint32_t v, uint32_t m)
 {
@@ -95,7 +111,7 @@ static void
 plan_chunks(uint32_t eblocks, unsigned ch, const bjxa_hip_tuning_t *t,
     struct plan *p)
 {
-	const uint32_t G = XA_CHUNK_Q(ch), lanes = target_lanes();
+	const uint32_t G = XA_CHUNK_Q(ch), lanes = plan_lanes(t);
 	const uint32_t w = (t && t->warmup >= 0) ? (uint32_t)t->warmup :
 	    DEFAULT_WARMUP;
 	uint32_t c;
@@ -489,7 +505,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		errno = ENODEV;
 		return NULL;
 	}
-	const uint32_t lanes = target_lanes();
+	const uint32_t lanes = plan_lanes(tune);
 	uint64_t cb = (cblocks + lanes - 1) / lanes;
 	if (tune && tune->chunk)
 		cb = tune->chunk;

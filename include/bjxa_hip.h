@@ -55,9 +55,13 @@ typedef struct {
 					 * wave leave its first boundary to
 					 * the sequential tail, bit 19 stops
 					 * waves waiting for the exit record
-					 * of the wave before them; other
-					 * bits reserved (0).  Pass the same
-					 * tuning to bjxa_hip_decode_workspace. */
+					 * of the wave before them; bit 20:
+					 * the caller keeps two decodes in
+					 * flight, plan for one decode-kernel
+					 * workgroup per CU (chunks twice as
+					 * long); other bits reserved (0).
+					 * Pass the same tuning to
+					 * bjxa_hip_decode_workspace. */
 } bjxa_hip_tuning_t;
 
 /*
