@@ -136,3 +136,19 @@ def test_manual_chunk_capped(built):
     assert status_state(st) == st_ref
     cap = ((1 << 32) - (1 << 20)) // (64 * 33 * 2) // 4 * 4
     assert st[6] == cap and st[5] == -(-eb // cap)
+
+
+def test_pipe2_plan(built):
+    """Tuning bit 20 (two decodes in flight): the planner targets half the
+    lanes, so the chunks are twice as long; bit-exact, including a ragged
+    tail and an entry state."""
+    eb = 2_500_003
+    frames = eb * 32 - 9
+    xa = synth.stream(eb, 8, 2, "A", seed=16)
+    ref, st_ref, _, _ = oracle.decode(xa, eb, 8, 2, (3, -3, 30, -30), frames)
+    got, st = dev_decode(xa, eb, 8, 2, frames=frames, state=(3, -3, 30, -30),
+                         want_status=True, variant=bjxa_amd.VARIANT_PIPE2)
+    assert np.array_equal(got, ref)
+    assert status_state(st) == st_ref
+    c = -(-(-(-eb // 65536)) // 4) * 4     # ceil(eb / (131072 / 2)) to the quantum
+    assert st[6] == c
