@@ -141,7 +141,10 @@ decode_eblock(const uint32_t *w, const int O, int32_t *p0, int32_t *p1,
 			u32x4a v = { fr[0], fr[1], fr[2], fr[3] };
 			constexpr int QL = LB / 16;	/* pieces per line */
 			const int qq = QB + q;
-			*(u32x4a *)(line + 16 * (RESTART ? (qq % QL) : qq)) = v;
+			/* (RESTART: the stage's piece order, pieces 4-7 of a
+			 * line 64 B further -- xa_decode.hip ost_piece) */
+			static_assert(!STORE || !RESTART || QL == 8, "stage piece order");
+			*(u32x4a *)(line + 16 * (RESTART ? (qq % QL) + (qq % QL & 4) : qq)) = v;
 			if (qq % QL == QL - 1)
 				flush(qq / QL);
 		}
