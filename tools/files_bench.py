@@ -4,7 +4,10 @@
 PCIe-inclusive by construction.  Median of 5 calls after a discarded first;
 every WAV checked against the oracle once.
 
-usage: python tools/files_bench.py [--files N]
+usage: python tools/files_bench.py [--files N] [--calls K]
+           [--libs label=path ...]   (interleaved A/B of library builds:
+                                      one call of each per round, in one
+                                      process; median per build)
 """
 import argparse
 import ctypes
@@ -26,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=1024)
     ap.add_argument("--calls", type=int, default=5)
+    ap.add_argument("--libs", nargs="*", default=None)
     args = ap.parse_args()
     files, samples = [], 0
     for i in range(args.files):
@@ -43,21 +47,34 @@ def main():
     wv_p = (ctypes.c_void_p * n)(*[ctypes.addressof(o) for o in outs])
     wv_l = (ctypes.c_size_t * n)(*[len(o) for o in outs])
     st = (ctypes.c_int * n)()
-    L = bjxa_amd.lib()
-    times = []
-    for _ in range(args.calls + 1):
-        t = time.perf_counter()
-        done = L.bjxa_hip_decode_files(xa_p, xa_l, wv_p, wv_l, st, n)
-        times.append(time.perf_counter() - t)
-        assert done == n, (done, list(st)[:8])
+    if args.libs:
+        libs = [(lab, ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL))
+                for lab, path in (x.split("=", 1) for x in args.libs)]
+    else:
+        libs = [("new", bjxa_amd.lib())]
     import oracle
-    ok = all(o.raw == oracle.decode_file(f) for o, f in zip(outs, files))
-    med = float(np.median(times[1:]))
+    want = [oracle.decode_file(f) for f in files]
+    times = {lab: [] for lab, _ in libs}
+    ok = {}
+    for r in range(args.calls + 1):
+        for lab, L in libs:
+            for o in outs:
+                ctypes.memset(o, 0, len(o))
+            t = time.perf_counter()
+            done = L.bjxa_hip_decode_files(xa_p, xa_l, wv_p, wv_l, st, n)
+            times[lab].append(time.perf_counter() - t)
+            assert done == n, (lab, done, list(st)[:8])
+            if r == 0:
+                ok[lab] = all(o.raw == w for o, w in zip(outs, want))
     moved = sum(len(f) for f in files) + sum(len(o) for o in outs)
-    print(json.dumps({"files": n, "samples": samples, "ms": round(med * 1e3, 2),
-                      "MSamples_per_s": round(samples / med / 1e6, 1),
-                      "host_GB_per_s": round(moved / med / 1e9, 2),
-                      "first_call_ms": round(times[0] * 1e3, 2), "bit_exact": ok}))
+    for lab, _ in libs:
+        med = float(np.median(times[lab][1:]))
+        print(json.dumps({"lib": lab, "files": n, "samples": samples,
+                          "ms": round(med * 1e3, 2),
+                          "MSamples_per_s": round(samples / med / 1e6, 1),
+                          "host_GB_per_s": round(moved / med / 1e9, 2),
+                          "first_call_ms": round(times[lab][0] * 1e3, 2),
+                          "bit_exact": ok[lab]}))
 
 
 if __name__ == "__main__":
