@@ -421,6 +421,23 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     elapsed, step_ms = timed_region(step, args.steps, depth, slots, dev)
 
     serial = timed_serial(step, args.steps, dev) if depth > 1 else elapsed
+    # diagnostic (BJXA_BENCH_RECAL=1): the calibration once more after the
+    # timed loops, to tell drift over the run from the window itself
+    recal = None
+    if os.environ.get("BJXA_BENCH_RECAL") == "1":
+        recal = choose_depth(step, len(slots), dev, 0)[1]
+        # the timed window's loop and the calibration's, interleaved
+        seq = []
+        for _ in range(3):
+            seq.append(("window", round(timed_region(step, args.steps, depth, slots,
+                                                      dev)[0] / args.steps * 1e3, 4)))
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                step(i if depth > 1 else 0)
+            torch.cuda.synchronize(dev)
+            seq.append(("loop", round((time.perf_counter() - t0) / args.steps * 1e3, 4)))
+        recal["interleaved"] = seq
 
     # kernel timing: slot 0 alone, one launch at a time (no overlap)
     evs = EventPairs(max(EV_SAMPLES, args.steps))
@@ -471,6 +488,7 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     xa_bytes = eb * ch * (bits * 4 + 1)
     return {"name": name, "desc": desc, "eb": eb, "bits": bits, "ch": ch, "samples": samples,
             "elapsed": elapsed, "serial": serial, "pipeline": depth, "pipeline_cal": cal,
+            "recal": recal,
             "step_ms": spread(step_ms, depth), "spec_ms": float(np.median(spec_ms)),
             "spec_samples": len(spec_ms), "status": st, "xa_bytes": xa_bytes,
             "alg_bytes": xa_bytes + eb * 64 * ch, "ok": ok, "pcm_equal_oracle": exact,
@@ -970,7 +988,8 @@ def main_stream(args, workload, dev, world, rank, others=None):
                    "profile_mix": args.mix, "parallelism": "independent streams, 1 per GPU",
                    "chunk": int(st[6]), "warmup_eblocks": int(st[7]),
                    "tuning": "auto" if not args.chunk and args.warm_blocks < 0 else "manual",
-                   "pipeline": r["pipeline"], "pipeline_cal": r["pipeline_cal"]},
+                   "pipeline": r["pipeline"], "pipeline_cal": r["pipeline_cal"],
+                   **({"recal": r["recal"]} if r.get("recal") else {})},
         "roofline": {"bound": "hbm", "kernel": "xa_decode_spec",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
