@@ -89,6 +89,26 @@ def test_repair_paths(built, chunk, warmup):
         assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
 
 
+@pytest.mark.parametrize("cut", [0, 8, 4, 3])
+def test_store_paths(built, cut):
+    """Each of K1's three store paths out of the LDS stage (xa_decode.hip
+    store_lines, ost_line / ost_piece / ost_quad): a stream whose last wave
+    is partial, ending on a whole block (cut 0) or inside its last block on
+    a 16-B boundary of the PCM (stereo cut 4 or 8 frames, mono cut 8) --
+    the predicated fast path -- or off it (cut 3, mono cut 4: per-piece
+    bounds and the 2-byte tail); every format, bit-exact."""
+    for bits in (4, 6, 8):
+        for ch in (1, 2):
+            eb = 64 * 40 * 3 + 40 * 5 + 17      # 3 whole waves, 5 chunks + 17 eblocks
+            xa = synth.stream(eb, bits, ch, "A", seed=900 + cut + bits + ch)
+            frames = eb * 32 - cut
+            ref, st_ref, _, _ = oracle.decode(xa, eb, bits, ch, frames=frames)
+            got, st = dev_decode(xa, eb, bits, ch, frames=frames, chunk=40,
+                                 want_status=True)
+            assert np.array_equal(got, ref), (bits, ch, cut)
+            assert status_state(st)[:2 * ch] == st_ref[:2 * ch]
+
+
 @pytest.mark.parametrize("eb", [1, 2, 3, 5, 31, 257])
 def test_tiny_streams(built, eb):
     for bits in (4, 6, 8):
