@@ -9,7 +9,9 @@
 #   ab=<wl>:<mix>[:<reps>[:<names>]]  tools/ab_inproc.py: this tree's library
 #                             against ab/<name>/libbjxa.so.0 for each name of the
 #                             comma list (default: every ab/*), interleaved in one
-#                             process
+#                             process (ab/ is in .gpurunignore so that the round's
+#                             GPU runs do not carry it: drop that line for an A/B
+#                             session)
 #   abx=<args>                tools/ab_inproc.py <args> as given (layouts, tunings)
 #   prof[=<args>]             tools/profile.sh <tag> <args> (trace + counter passes)
 #   ktrace=<wl>:<mix>:<names> rocprofv3 --kernel-trace over tools/ab_inproc.py, one
