@@ -330,18 +330,9 @@ PIPE_CAL_ROUNDS = 4     # interleaved runs per depth
 PIPE_CAL_MARGIN = 0.01  # two in flight must win by this much
 
 
-def choose_depth(step, nslots, dev, want):
-    """Steps in flight for the timed region.  want >= 1: that many (up to
-    the slots made).  want == 0 (auto, the default): after the warm-up,
-    PIPE_CAL_STEPS steps one at a time and the same with every slot in
-    flight, PIPE_CAL_ROUNDS times each, interleaved; steps in flight are
-    timed only if every run of them beats every run one at a time by
-    PIPE_CAL_MARGIN
-    (round 2: two in flight won 4 % on C3 and lost 3-10 % on C4/C5g on the
-    driver's box; on C3 the two are often within noise).  Returns (depth,
-    median calibration ms per step, or None)."""
-    if want >= 1 or nslots == 1:
-        return max(1, min(want, nslots)), None
+def calibration_pass(step, nslots, dev):
+    """PIPE_CAL_ROUNDS runs of PIPE_CAL_STEPS steps one at a time and with
+    every slot in flight, interleaved; wall seconds of each run per depth."""
     import torch
     t = {1: [], nslots: []}
     for _ in range(PIPE_CAL_ROUNDS):
@@ -352,6 +343,27 @@ def choose_depth(step, nslots, dev, want):
                 step(i if d > 1 else 0)
             torch.cuda.synchronize(dev)
             t[d].append(time.perf_counter() - t0)
+    return t
+
+
+def choose_depth(step, nslots, dev, want):
+    """Steps in flight for the timed region.  want >= 1: that many (up to
+    the slots made).  want == 0 (auto, the default): after the warm-up,
+    PIPE_CAL_STEPS steps one at a time and the same with every slot in
+    flight, PIPE_CAL_ROUNDS times each, interleaved, in two passes of which
+    the second decides (the first settles the GPU); steps in flight are
+    timed only if every run of them beats every run one at a time by
+    PIPE_CAL_MARGIN
+    (round 2: two in flight won 4 % on C3 and lost 3-10 % on C4/C5g on the
+    driver's box; on C3 the two are often within noise).  Returns (depth,
+    median calibration ms per step, or None)."""
+    if want >= 1 or nslots == 1:
+        return max(1, min(want, nslots)), None
+    # the first pass only settles the GPU: a timed window right after a
+    # single pass ran 0.5-3 % slower on C3 and 2-8 % on C2, whose second
+    # pass also shows two in flight winning (DESIGN.md §5 R5-2)
+    calibration_pass(step, nslots, dev)
+    t = calibration_pass(step, nslots, dev)
     med = {d: float(np.median(v)) for d, v in t.items()}
     # steps in flight only if their slowest run beats the fastest run one at
     # a time: how two in-flight steps interleave depends on host timing, and
