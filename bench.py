@@ -330,6 +330,17 @@ PIPE_CAL_ROUNDS = 4     # interleaved runs per depth
 PIPE_CAL_MARGIN = 0.01  # two in flight must win by this much
 
 
+def py_median(v):
+    """Median in plain Python.  Not numpy: a numpy call just before the
+    timed window slowed it by 3 % on C3 and 15 % on C4 (and the
+    one-at-a-time pass after it), reproducibly, against the same code with
+    this helper; nothing numpy runs between the
+    calibration and the timed loops."""
+    s = sorted(v)
+    n = len(s)
+    return (s[(n - 1) // 2] + s[n // 2]) / 2.0
+
+
 def calibration_pass(step, nslots, dev):
     """PIPE_CAL_ROUNDS runs of PIPE_CAL_STEPS steps one at a time and with
     every slot in flight, interleaved; wall seconds of each run per depth."""
@@ -364,7 +375,7 @@ def choose_depth(step, nslots, dev, want):
     # pass also shows two in flight winning
     calibration_pass(step, nslots, dev)
     t = calibration_pass(step, nslots, dev)
-    med = {d: float(np.median(v)) for d, v in t.items()}
+    med = {d: py_median(v) for d, v in t.items()}
     # steps in flight only if their slowest run beats the fastest run one at
     # a time: how two in-flight steps interleave depends on host timing, and
     # a config whose runs spread (C4: 0.45-0.51 ms) is
