@@ -67,6 +67,16 @@ def test_bench_reduction_world2():
         assert hs[0] != hs[1]                   # ranks decode different streams
 
 
+def test_py_median():
+    """bench.py's calibration median (plain Python, so that no numpy call
+    runs between the calibration and the timed loops) equals numpy's."""
+    import bench
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 3, 4, 7, 8):
+        v = list(rng.random(n))
+        assert bench.py_median(v) == pytest.approx(float(np.median(v)))
+
+
 def test_job_value_weak_scaling():
     import bench
     # 2 ranks x 320M samples x 20 steps in 10 ms
