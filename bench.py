@@ -331,11 +331,11 @@ PIPE_CAL_MARGIN = 0.01  # two in flight must win by this much
 
 
 def py_median(v):
-    """Median in plain Python.  Not numpy: a numpy call just before the
-    timed window slowed it by 3 % on C3 and 15 % on C4 (and the
-    one-at-a-time pass after it), reproducibly, against the same code with
-    this helper; nothing numpy runs between the
-    calibration and the timed loops."""
+    """Median in plain Python.  Not numpy: the first np.median of a process
+    pauses the host ~8 ms (lazy imports), and a GPU left idle that long
+    before the timed window ran it 3 % slower on C3 and 15 % on C4 (and
+    the one-at-a-time pass after it), reproducibly (DESIGN.md §5 R5-2);
+    nothing numpy runs between the calibration and the timed loops."""
     s = sorted(v)
     n = len(s)
     return (s[(n - 1) // 2] + s[n // 2]) / 2.0
