@@ -77,6 +77,23 @@ def test_py_median():
         assert bench.py_median(v) == pytest.approx(float(np.median(v)))
 
 
+def test_choose_depth_calls_no_numpy(monkeypatch):
+    """choose_depth ends right before the timed window, so it must not call
+    numpy (a first numpy call pauses the host and idles the GPU, DESIGN.md
+    §5 R5-2): run it on CPU with numpy's reductions made to fail."""
+    import bench
+
+    def boom(*a, **k):
+        raise AssertionError("numpy called in choose_depth")
+    for name in ("median", "mean", "percentile", "min", "max", "sort"):
+        monkeypatch.setattr(bench.np, name, boom)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    calls = []
+    depth, cal = bench.choose_depth(lambda i: calls.append(i), 2, torch.device("cpu"), 0)
+    assert depth in (1, 2) and len(calls) == 2 * bench.PIPE_CAL_ROUNDS * 2 * bench.PIPE_CAL_STEPS
+    assert len(cal["runs_ms"]["depth1"]) == bench.PIPE_CAL_ROUNDS
+
+
 def test_job_value_weak_scaling():
     import bench
     # 2 ranks x 320M samples x 20 steps in 10 ms
