@@ -448,7 +448,8 @@ def run_workload(name, args, dev, world, rank, verify, cpu_leg):
     # timed loops, to tell drift over the run from the window itself
     recal = None
     if os.environ.get("BJXA_BENCH_RECAL") == "1":
-        recal = choose_depth(step, len(slots), dev, 0)[1]
+        # (with one slot there is nothing to calibrate: choose_depth gives None)
+        recal = choose_depth(step, len(slots), dev, 0)[1] or {}
         # the timed window's loop and the calibration's, interleaved
         seq = []
         for _ in range(3):

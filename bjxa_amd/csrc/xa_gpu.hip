@@ -182,6 +182,67 @@ ws_bytes(uint32_t nchunks)
 	return ws_exits_off(nchunks) + (size_t)(nchunks + 63) / 64 * 16 + 64;
 }
 
+/*
+ * The exit records are recognised by their launch tag alone (xa_decode.hip
+ * put_exit/get_exit).  The tag is a small counter, so the record region must
+ * not hold words another use of the memory left behind: the g/e states and
+ * queue entries of a decode with another layout (a smaller stream in a
+ * workspace sized for a larger one puts its records on them) are small
+ * integers too, and a stale pair equal to the tag would pass as the wave
+ * before's exit.  After bjxa_hip_workspace_init the region is zero, and it
+ * stays records while the workspace keeps its layout; a decode whose record
+ * region differs from the last one on the same workspace zeroes its region
+ * first (a stream-ordered memset of 16 B per wave).  Remembered per
+ * workspace address; a workspace this table has forgotten is zeroed too.
+ */
+#define WS_SEEN		64
+#define WS_ZEROED	((size_t)-1)	/* whole workspace zero (just initialised) */
+
+static std::mutex ws_seen_mu;
+static struct {
+	const void	*ws;
+	size_t		off;		/* record region: byte offset, length */
+	size_t		len;
+} ws_seen[WS_SEEN];
+static unsigned ws_seen_next;
+
+/* record that workspace ws now has its records at [off, off + len); true if
+ * that region may hold words of another layout (it must be zeroed) */
+static bool
+ws_records_stale(const void *ws, size_t off, size_t len)
+{
+	std::lock_guard<std::mutex> lk(ws_seen_mu);
+	for (unsigned i = 0; i < WS_SEEN; i++) {
+		if (ws_seen[i].ws != ws)
+			continue;
+		const bool same = ws_seen[i].off == WS_ZEROED ||
+		    (ws_seen[i].off == off && ws_seen[i].len == len);
+		ws_seen[i].off = off;
+		ws_seen[i].len = len;
+		return !same;
+	}
+	const unsigned i = ws_seen_next++ % WS_SEEN;
+	ws_seen[i].ws = ws;
+	ws_seen[i].off = off;
+	ws_seen[i].len = len;
+	return true;
+}
+
+static void
+ws_records_zeroed(const void *ws)
+{
+	std::lock_guard<std::mutex> lk(ws_seen_mu);
+	for (unsigned i = 0; i < WS_SEEN; i++)
+		if (ws_seen[i].ws == ws) {
+			ws_seen[i].off = WS_ZEROED;
+			return;
+		}
+	const unsigned i = ws_seen_next++ % WS_SEEN;
+	ws_seen[i].ws = ws;
+	ws_seen[i].off = WS_ZEROED;
+	ws_seen[i].len = 0;
+}
+
 extern "C" size_t
 bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
     const bjxa_hip_tuning_t *tune)
@@ -223,6 +284,7 @@ bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream)
 		errno = EIO;
 		return -1;
 	}
+	ws_records_zeroed(d_ws);
 	return 0;
 }
 
@@ -276,6 +338,14 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	a.tag = 0;	/* set per launch */
 	verify_knobs(tune, &a.spin, &a.flags);
 	a.status = d_status;
+	const size_t xlen = (size_t)(p.nchunks + 63) / 64 * 16;
+	if (ws_records_stale(d_ws, ws_exits_off(p.nchunks), xlen) &&
+	    hipMemsetAsync(a.exits, 0, xlen, (hipStream_t)stream) != hipSuccess) {
+		(void)hipGetLastError();
+		(void)ws_records_stale(d_ws, 0, 0);	/* no region: zero next time */
+		errno = EIO;
+		return -1;
+	}
 	hipEvent_t e0 = tune ? (hipEvent_t)tune->ev_spec[0] : NULL;
 	hipEvent_t e1 = tune ? (hipEvent_t)tune->ev_spec[1] : NULL;
 	const hipError_t rc = xa_decode_launch(a, s->bits, s->channels,

@@ -230,7 +230,10 @@ def run_packed(specs, chunk, layout, variant=0):
                 PACKED_SPAN bytes (a caller's own big buffer)
       "raw"     a hipMalloc of its own each
       "torch"   a torch tensor each (small ones share the caching
-                allocator's segments)"""
+                allocator's segments)
+      "carved"  a torch tensor each, carved by the caching allocator out of
+                one freed block of 128 MiB (so one allocation of >= 64 MiB,
+                at offsets the allocator chose)"""
     torch = require_gpu()
     sizes = [eb * 64 * ch for _, eb, _, ch, _, _ in specs]
     with RawBuffers() as raw:
@@ -241,6 +244,12 @@ def run_packed(specs, chunk, layout, variant=0):
             dsts = [big[o:o + n] for o, n in zip(offs, sizes)]
         elif layout == "raw":
             dsts = [raw.get(n) for n in sizes]
+        elif layout == "carved":
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            big = torch.empty((128 << 20,), dtype=torch.uint8, device="cuda")
+            del big                     # cached, free: the next tensors split it
+            dsts = [torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda") for n in sizes]
         else:
             dsts = [torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda") for n in sizes]
         srcs = [torch.from_numpy(np.ascontiguousarray(xa)).cuda() for xa, *_ in specs]
@@ -258,20 +267,25 @@ def run_packed(specs, chunk, layout, variant=0):
     return out, status.cpu().numpy().view(np.uint32).reshape(len(specs), -1).copy()
 
 
-@pytest.mark.parametrize("layout", ["raw", "torch", "packed"])
+@pytest.mark.parametrize("layout", ["raw", "torch", "packed", "carved"])
 def test_batch_packed_layout_plan(built, layout):
     """Streams whose PCM lane stride is a multiple of 8 KiB (here 64 stereo
     eblocks per lane) get chunks one quantum longer only when eight or more
     PCM images share one allocation of at least 64 MiB (a caller's packed
     buffer); in allocations of their own, and in torch tensors that share
     the caching allocator's (smaller) segments, they keep them (DESIGN.md §5
-    R4-7, R5-4).  Bit-exact either way, including with the choice forced off
-    and on."""
-    specs = [make(4096, 8, 2, 900 + i, cut=(5 if i == 3 else 0)) for i in range(8)]
-    pcms, st = run_packed(specs, 128, layout)
+    R4-7, R5-4).  Tensors the caching allocator carves out of one freed
+    block of >= 64 MiB share that allocation as a packed buffer does, and R4-11
+    measured one allocation to want the longer chunks whatever the offsets
+    between its images, so they count as packed.  Bit-exact
+    either way, including with the choice forced off and on."""
+    eb = 16384 if layout == "carved" else 4096      # 2 MiB PCM: the large pool
+    specs = [make(eb, 8, 2, 900 + i, cut=(5 if i == 3 else 0)) for i in range(8)]
+    chunk = 128
+    pcms, st = run_packed(specs, chunk, layout)
     check(specs, pcms, st)
-    assert (st[:, 6] == (68 if layout == "packed" else 64)).all()
+    assert (st[:, 6] == (68 if layout in ("packed", "carved") else 64)).all()
     for v, c in ((bjxa_amd.VARIANT_NODECOR, 64), (bjxa_amd.VARIANT_DECOR, 68)):
-        pcms, st = run_packed(specs, 128, layout, v)
+        pcms, st = run_packed(specs, chunk, layout, v)
         check(specs, pcms, st)
         assert (st[:, 6] == c).all()

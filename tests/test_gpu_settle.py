@@ -109,6 +109,61 @@ def test_stale_workspace(built, poke):
     assert np.array_equal(got, ref)
 
 
+def test_smaller_stream_reuses_workspace(built):
+    """a smaller stream decoded in a workspace sized for (and
+    last used by) a larger one puts its exit records on the larger decode's
+    stale g/e/queue words.  Records pass on their launch tag alone, and the
+    tag is a small counter, so the worst case is written here: every stale
+    word pair in the smaller layout's record region set to the NEXT launch's
+    tag with a bogus state beside it.  The library zeroes a record region
+    whose layout changed (xa_gpu.hip ws_records_stale); without that, lane
+    0 of every wave would repair its chunk from the bogus state."""
+    torch = require_gpu()
+    big, small, bits, ch = 3_000_000, 900_000, 8, 2
+    xa_big = synth.stream(big, bits, ch, "A", seed=17)
+    xa_small = synth.stream(small, bits, ch, "W", seed=18)
+    ref_big, _, _, _ = oracle.decode(xa_big, big, bits, ch)
+    ref_small, st_ref, _, _ = oracle.decode(xa_small, small, bits, ch)
+    ws_len = bjxa_amd.decode_workspace_size(big, ch, 0, 0)
+    ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    bjxa_amd.workspace_init(ws.data_ptr(), ws_len, sh)
+
+    def decode(xa, eb):
+        src = torch.from_numpy(xa).cuda()
+        dst = torch.full((eb * 64 * ch,), 0x5A, dtype=torch.uint8, device="cuda")
+        bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, bits, ch,
+                               ws.data_ptr(), ws_len, status.data_ptr(), (0, 0, 0, 0),
+                               0, 0, sh)
+        torch.cuda.synchronize()
+        return dst.cpu().numpy().view(np.int16), status.cpu().numpy().view(np.uint32).copy()
+
+    got, st = decode(xa_small, small)          # learn the smaller layout
+    assert np.array_equal(got, ref_small)
+    n_small = int(st[5])
+    got, st = decode(xa_big, big)
+    assert np.array_equal(got, ref_big)
+    n_big = int(st[5])
+    assert n_big > n_small
+    xb = _layout(n_big)[3]
+    rec = ws[xb:xb + 16].cpu().numpy().view(np.uint32)
+    assert rec[1] == rec[3] != 0               # {state, tag} x 2: this launch's tag
+    nxt = (int(rec[1]) + 1) & 0xFFFFFFFF or 1
+    xs = _layout(n_small)[3]
+    nw = (n_small + 63) // 64
+    assert xs + 16 * nw <= _layout(n_big)[3]   # inside the big decode's g/e/queue
+    words = np.empty((nw, 4), dtype=np.uint32)
+    words[:, 0::2] = 0x12345678                # bogus exit state, both channels
+    words[:, 1::2] = nxt
+    ws[xs:xs + 16 * nw].copy_(torch.from_numpy(words.reshape(-1).view(np.uint8)))
+    got, st = decode(xa_small, small)
+    assert np.array_equal(got, ref_small)
+    assert status_state(st) == st_ref
+    rec = ws[xs:xs + 16].cpu().numpy().view(np.uint32)
+    assert rec[1] == rec[3] == nxt             # the tag prediction held
+
+
 @pytest.mark.parametrize("variant", [bjxa_amd.VARIANT_NORECORD, bjxa_amd.VARIANT_NOWAIT])
 def test_batch_boundaries_left_to_tail(built, variant):
     """The batch kernel with the same knobs: every format, cascades."""

@@ -1,0 +1,177 @@
+/*
+ * write_probe2.hip -- where does the write ceiling of MI355X_MICROARCH.md
+ * (plain stores 6.0-6.2 TB/s: one dword per lane, 256 B per
+ * wave-instruction, random 2,304-B rows of a 75 MB or 302 MB table, 8 waves
+ * per CU) part from the ~5 TB/s K1's output and tools/write_probe.hip see?
+ * 
+ *
+ * One kernel shape, changed one factor at a time: 512 workgroups of 256
+ * threads (8 waves per CU on 256 CUs, K1's occupancy); wave w writes rows
+ * rows[w * rpw .. w * rpw + rpw - 1] of `row` bytes each, every row swept by
+ * consecutive wave-instructions of `width` bytes per lane (4: 256 B per
+ * instruction; 16: 1 KiB); rows in random order (a permutation, every row
+ * written once per launch) or in order.  Factors: table size, width, row
+ * length, order, store policy (plain / nt), and whether each timed launch
+ * follows a 1 GiB read that evicts the 256 MiB Infinity Cache ("flush": the
+ * table's dirty lines of the previous launch are written back before the
+ * timed launch, not during it) or follows the previous launch directly
+ * ("warm", which is how a back-to-back loop times it).
+ *
+ * Prints one JSON line per case: median ms of 10 launches, TB/s of the
+ * bytes the launch stores.
+ *
+ * build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/bin/write_probe2 \
+ *            tools/write_probe2.hip
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <numeric>
+#include <random>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+	fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+#define WGS	512
+#define WAVES	(WGS * 4)
+
+template <int WIDTH, int NT>
+__global__ __launch_bounds__(256) void
+kw(uint8_t *out, const uint32_t *rows, uint32_t rpw, uint32_t row)
+{
+	const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63u;
+	const u32x4 v4 = { lane, w, 1u, 2u };
+	for (uint32_t r = 0; r < rpw; r++) {
+		uint8_t *base = out + (uint64_t)rows[w * rpw + r] * row;
+		for (uint32_t o = lane * WIDTH; o < row; o += 64u * WIDTH) {
+			if (WIDTH == 16) {
+				if (NT)
+					__builtin_nontemporal_store(v4, (u32x4 *)(base + o));
+				else
+					*(u32x4 *)(base + o) = v4;
+			} else {
+				if (NT)
+					__builtin_nontemporal_store(w + lane, (uint32_t *)(base + o));
+				else
+					*(uint32_t *)(base + o) = w + lane;
+			}
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void
+kflush(const u32x4 *in, uint64_t n, uint32_t *sink)
+{
+	u32x4 acc = { 0u, 0u, 0u, 0u };
+	for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull)
+		acc ^= in[i];
+	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u)
+		sink[0] = 1u;	/* practically never: keeps the loads */
+}
+
+struct cfg {
+	const char *name;
+	uint64_t table;		/* bytes */
+	uint32_t row, width;
+	bool random, nt, flush;
+};
+
+static uint8_t *g_out;
+static u32x4 *g_fl;
+static uint32_t *g_sink;
+#define FLUSH_BYTES (1ull << 30)
+
+static void
+run(const cfg &c)
+{
+	const uint32_t nrows = (uint32_t)(c.table / c.row);
+	const uint32_t rpw = nrows / WAVES;
+	const uint32_t n = rpw * WAVES;
+	std::vector<uint32_t> h(n);
+	std::iota(h.begin(), h.end(), 0u);
+	if (c.random) {
+		std::mt19937 rng(12345);
+		std::shuffle(h.begin(), h.end(), rng);
+	}
+	uint32_t *d;
+	CHECK(hipMalloc(&d, (size_t)n * 4));
+	CHECK(hipMemcpy(d, h.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+	hipEvent_t a, b;
+	CHECK(hipEventCreate(&a));
+	CHECK(hipEventCreate(&b));
+	std::vector<float> ms;
+	for (int it = 0; it < 13; it++) {
+		if (c.flush)
+			hipLaunchKernelGGL(kflush, dim3(2048), dim3(256), 0, 0, g_fl,
+			    FLUSH_BYTES / 16, g_sink);
+		CHECK(hipEventRecord(a, 0));
+#define L(W, N) hipLaunchKernelGGL((kw<W, N>), dim3(WGS), dim3(256), 0, 0, g_out, d, rpw, c.row)
+		if (c.width == 16)
+			c.nt ? L(16, 1) : L(16, 0);
+		else
+			c.nt ? L(4, 1) : L(4, 0);
+#undef L
+		CHECK(hipEventRecord(b, 0));
+		CHECK(hipEventSynchronize(b));
+		float t;
+		CHECK(hipEventElapsedTime(&t, a, b));
+		if (it >= 3)
+			ms.push_back(t);
+	}
+	std::sort(ms.begin(), ms.end());
+	const double bytes = (double)n * c.row;
+	printf("{\"case\": \"%s\", \"table_MB\": %.1f, \"row\": %u, \"width\": %u, "
+	    "\"order\": \"%s\", \"policy\": \"%s\", \"before\": \"%s\", \"ms\": %.4f, "
+	    "\"ms_min\": %.4f, \"ms_max\": %.4f, \"write_TBps\": %.3f}\n", c.name,
+	    bytes / 1e6, c.row, c.width, c.random ? "random" : "in order",
+	    c.nt ? "nt" : "plain", c.flush ? "1 GiB read" : "previous launch",
+	    ms[ms.size() / 2], ms.front(), ms.back(), bytes / ms[ms.size() / 2] / 1e9);
+	fflush(stdout);
+	CHECK(hipFree(d));
+	CHECK(hipEventDestroy(a));
+	CHECK(hipEventDestroy(b));
+}
+
+int
+main()
+{
+	CHECK(hipMalloc(&g_out, 1300ull << 20));
+	CHECK(hipMalloc(&g_fl, FLUSH_BYTES));
+	CHECK(hipMalloc(&g_sink, 64));
+	CHECK(hipMemset(g_fl, 1, FLUSH_BYTES));
+	CHECK(hipMemset(g_out, 0, 1300ull << 20));
+	const uint64_t T75 = 32768ull * 2304, T302 = 131072ull * 2304,
+	    T642 = 642ull << 20, T1200 = 1200ull << 20;
+	const cfg cases[] = {
+		/* the guide's row, as it reads */
+		{ "guide", T302, 2304, 4, true, false, false },
+		{ "guide_75MB", T75, 2304, 4, true, false, false },
+		/* one factor at a time from it */
+		{ "flush", T302, 2304, 4, true, false, true },
+		{ "642MB", T642, 2304, 4, true, false, false },
+		{ "642MB_flush", T642, 2304, 4, true, false, true },
+		{ "in_order", T302, 2304, 4, false, false, false },
+		{ "in_order_flush", T302, 2304, 4, false, false, true },
+		{ "16B", T302, 2304, 16, true, false, false },
+		{ "16B_flush", T302, 2304, 16, true, false, true },
+		{ "nt", T302, 2304, 4, true, true, false },
+		{ "nt_flush", T302, 2304, 4, true, true, true },
+		/* towards K1's output: 642 MB once per launch, 16 B per lane,
+		 * in order (its lines go out front to back per chunk), nt */
+		{ "k1ish_plain", T642, 2048, 16, false, false, true },
+		{ "k1ish_nt", T642, 2048, 16, false, true, true },
+		{ "k1ish_nt_warm", T642, 2048, 16, false, true, false },
+		{ "k1ish_nt_random", T642, 2048, 16, true, true, true },
+		{ "1.2GB_plain", T1200, 2048, 16, false, false, true },
+		{ "1.2GB_nt", T1200, 2048, 16, false, true, true },
+	};
+	for (int rep = 0; rep < 2; rep++)
+		for (const cfg &c : cases)
+			run(c);
+	return 0;
+}
