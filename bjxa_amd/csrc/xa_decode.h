@@ -109,8 +109,6 @@ struct xa_batch_stream {		/* 64 B, device table entry */
 struct xa_batch_args {
 	const xa_batch_stream *streams;
 	const uint32_t *wstream;	/* stream of each wave */
-	const uint32_t *worder;		/* grid position -> wave (NULL: the
-					 * identity; xa_gpu.hip batch_order) */
 	uint32_t nstreams, nwaves;	/* global chunks = 64 * nwaves */
 	uint32_t W;
 	uint32_t pace;			/* as xa_dec_args::pace */

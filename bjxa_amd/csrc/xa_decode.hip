@@ -1197,19 +1197,15 @@ xa_decode_spec_batch(xa_batch_args b)
 	    lds[XA_SPEC_WPB * batch_lds::REGION];
 	const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int lane = threadIdx.x & 63;
-	/* grid position -> wave (the host's balanced order, or the identity) */
-	auto wave_at = [&](uint32_t gp) {
-		return b.worder != nullptr ? b.worder[gp] : gp;
-	};
-	const uint32_t gw = blockIdx.x * XA_SPEC_WPB + wv;
+	const uint32_t w = blockIdx.x * XA_SPEC_WPB + wv;
 	/* lockstep (spec_wave2's pacing) only when all the workgroup's waves
 	 * exist and run the same number of super-steps: same chunk length and
 	 * channel count */
 	const uint32_t w0 = blockIdx.x * XA_SPEC_WPB;
 	bool lockstep = b.pace != 0u && w0 + XA_SPEC_WPB <= b.nwaves;
 	if (lockstep) {
-		auto shape = [&](uint32_t gp) {
-			const xa_batch_stream &d = b.streams[b.wstream[wave_at(gp)]];
+		auto shape = [&](uint32_t wk) {
+			const xa_batch_stream &d = b.streams[b.wstream[wk]];
 			return (b.W + d.C) | (d.fmt >> 8) << 24;
 		};
 		const uint32_t s0 = shape(w0);
@@ -1217,9 +1213,8 @@ xa_decode_spec_batch(xa_batch_args b)
 			lockstep = lockstep && shape(w0 + k) == s0;
 	}
 	lockstep = __builtin_amdgcn_readfirstlane(lockstep);
-	if (gw >= b.nwaves)
+	if (w >= b.nwaves)
 		return;
-	const uint32_t w = __builtin_amdgcn_readfirstlane(wave_at(gw));
 	const uint32_t sid = __builtin_amdgcn_readfirstlane(b.wstream[w]);
 	const xa_dec_args a = batch_stream_args(b, sid);
 	const uint32_t fmt = __builtin_amdgcn_readfirstlane(b.streams[sid].fmt);

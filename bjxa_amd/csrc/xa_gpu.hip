@@ -534,129 +534,6 @@ packed_pcm(const bjxa_hip_stream_t *s, uint32_t n, const bjxa_hip_tuning_t *t)
 }
 
 /*
- * Grid order of a batch's waves (xa_batch_args::worder; experimental,
- * tuning variant bits 22/23).  The planner gives every
- * lane about the same channel blocks, but whole waves per stream do not
- * make every lane's work equal: in C4 a mono stream of 16,384 blocks gets
- * one wave of 256 blocks per lane, a stereo one three waves of 88 eblocks
- * (176 channel blocks), and in stream order a third of the workgroups hold
- * three mono waves and the rest none.  The waves are grouped into classes
- * of equal lane cost (format and chunk length); bit 22 deals them into the
- * grid so that every class is spread evenly over it (each grid position
- * takes the class furthest behind its proportional share: every workgroup
- * gets the same mix), bit 23 puts the costliest class first.  Within a
- * class the waves keep their order, so a stream's waves stay in grid order
- * -- a wave never waits on the exit record of a wave dispatched after it.
- * Returns NULL (grid order = stream order, the default) when no bit is set
- * or all waves cost the same; else a malloc'ed array of nwaves slot-wave
- * indices.
- */
-#define XA_VARIANT_SPREAD	0x400000u
-#define XA_VARIANT_CLUSTER	0x800000u
-#define ORDER_CLASSES		16
-
-static uint32_t *
-batch_order(const xa_batch_stream *hs, const uint32_t *hw,
-    uint32_t nwaves, uint32_t W, const bjxa_hip_tuning_t *t, int *nomem)
-{
-	*nomem = 0;
-	const uint32_t v = t ? t->variant : 0u;
-	if (!(v & (XA_VARIANT_SPREAD | XA_VARIANT_CLUSTER)) || nwaves < 8u)
-		return NULL;
-	/* classes: (fmt, C) pairs; a lane's bytes as the cost */
-	uint32_t key[ORDER_CLASSES], cnt[ORDER_CLASSES] = { 0 };
-	uint64_t cost[ORDER_CLASSES];
-	int nk = 0;
-	uint8_t *cls = (uint8_t *)malloc(nwaves);
-	if (cls == NULL) {
-		*nomem = 1;
-		return NULL;
-	}
-	for (uint32_t w = 0; w < nwaves; w++) {
-		const xa_batch_stream &d = hs[hw[w]];
-		const uint32_t k = d.fmt | d.C << 16;
-		int j = 0;
-		while (j < nk && key[j] != k)
-			j++;
-		if (j == nk) {
-			if (nk == ORDER_CLASSES) {	/* too varied: keep stream order */
-				free(cls);
-				return NULL;
-			}
-			const uint64_t bits = d.fmt & 0xffu, ch = d.fmt >> 8;
-			key[nk] = k;
-			cost[nk] = ((uint64_t)d.C + W) * ch * (4 * bits + 1) +
-			    (uint64_t)d.C * ch * 64;
-			nk++;
-		}
-		cls[w] = (uint8_t)j;
-		cnt[j]++;
-	}
-	uint64_t lo = cost[0], hi = cost[0];
-	for (int j = 1; j < nk; j++) {
-		lo = cost[j] < lo ? cost[j] : lo;
-		hi = cost[j] > hi ? cost[j] : hi;
-	}
-	if (nk < 2 || hi * 10 < lo * 11) {	/* within 10 %: nothing to spread */
-		free(cls);
-		return NULL;
-	}
-	/* each class's waves in slot order */
-	uint32_t start[ORDER_CLASSES], taken[ORDER_CLASSES] = { 0 };
-	uint32_t *byc = (uint32_t *)malloc((size_t)nwaves * 4);
-	uint32_t *ord = (uint32_t *)malloc((size_t)nwaves * 4);
-	if (byc == NULL || ord == NULL) {
-		free(cls);
-		free(byc);
-		free(ord);
-		*nomem = 1;
-		return NULL;
-	}
-	for (int j = 0, o = 0; j < nk; o += cnt[j], j++)
-		start[j] = o;
-	{
-		uint32_t fill[ORDER_CLASSES];
-		memcpy(fill, start, sizeof fill);
-		for (uint32_t w = 0; w < nwaves; w++)
-			byc[fill[cls[w]]++] = w;
-	}
-	if (v & XA_VARIANT_CLUSTER) {
-		/* classes by cost, costliest first */
-		for (uint32_t g = 0; g < nwaves;) {
-			int best = -1;
-			for (int j = 0; j < nk; j++)
-				if (taken[j] < cnt[j] && (best < 0 || cost[j] > cost[best]))
-					best = j;
-			for (; taken[best] < cnt[best]; taken[best]++)
-				ord[g++] = byc[start[best] + taken[best]];
-		}
-		free(cls);
-		free(byc);
-		return ord;
-	}
-	/* grid position g takes the class whose share of positions 0..g is
-	 * furthest ahead of what it has had: cnt*(g+1)/nwaves - taken */
-	for (uint32_t g = 0; g < nwaves; g++) {
-		int best = -1;
-		int64_t bd = 0;
-		for (int j = 0; j < nk; j++) {
-			if (taken[j] == cnt[j])
-				continue;
-			const int64_t d = (int64_t)cnt[j] * (g + 1) -
-			    (int64_t)taken[j] * nwaves;
-			if (best < 0 || d > bd) {
-				best = j;
-				bd = d;
-			}
-		}
-		ord[g] = byc[start[best] + taken[best]++];
-	}
-	free(cls);
-	free(byc);
-	return ord;
-}
-
-/*
  * Plan: one budget of channel blocks per lane, Cb = the batch's channel
  * blocks / target_lanes() (at least MIN_CHUNK, a multiple of 4); a stream of
  * E eblocks and ch channels gets k = round(E*ch / (64*Cb)) >= 1 whole
@@ -757,9 +634,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 		errno = EINVAL;
 		return NULL;
 	}
-	/* hw: the stream of each wave, then (if not stream order) the grid
-	 * order of the waves */
-	uint32_t *hw = (uint32_t *)malloc(nwaves * 8);
+	uint32_t *hw = (uint32_t *)malloc(nwaves * 4);
 	bjxa_hip_batch_t *b = (bjxa_hip_batch_t *)calloc(1, sizeof *b);
 	if (hw == NULL || b == NULL) {
 		free(hs);
@@ -771,27 +646,12 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	for (uint32_t i = 0, wv = 0; i < n; i++)
 		for (uint32_t j = 0; j < (hs[i].nchunks + 63) / 64; j++)
 			hw[wv++] = i;
-	int nomem;
-	uint32_t *ord = batch_order(hs, hw, (uint32_t)nwaves, W, tune, &nomem);
-	if (nomem) {
-		free(hs);
-		free(hw);
-		free(b);
-		errno = ENOMEM;
-		return NULL;
-	}
-	const bool ordered = ord != NULL;
-	if (ordered) {
-		memcpy(hw + nwaves, ord, nwaves * 4);
-		free(ord);
-	}
-	const size_t hw_words = ordered ? 2 * nwaves : nwaves;
 
 	const size_t nc = 64 * nwaves;
 	const size_t o_sctl = al64(XA_CTL_WORDS * 4);
 	const size_t o_str = o_sctl + al64((size_t)n * XA_SCTL_WORDS * 4);
 	const size_t o_wav = o_str + al64((size_t)n * sizeof(xa_batch_stream));
-	const size_t o_g = o_wav + al64(nwaves * 8);
+	const size_t o_g = o_wav + al64(nwaves * 4);
 	const size_t o_e = o_g + nc * 8;
 	const size_t o_q = o_e + nc * 8;
 	const size_t o_x = al64(o_q + 2 * nc * 4);	/* exit records */
@@ -834,7 +694,6 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	xa_batch_args &a = b->args;
 	a.streams = (const xa_batch_stream *)(ws + o_str);
 	a.wstream = (const uint32_t *)(ws + o_wav);
-	a.worder = ordered ? (const uint32_t *)(ws + o_wav) + nwaves : NULL;
 	a.nstreams = n;
 	a.nwaves = (uint32_t)nwaves;
 	a.W = W;
@@ -854,7 +713,7 @@ bjxa__batch_new(const bjxa_hip_stream_t *s, uint32_t n,
 	 * earlier batch on the same stream (the files path) */
 	int bad = hipMemcpyAsync(ws + o_str, hs, (size_t)n * sizeof *hs,
 	    hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess ||
-	    hipMemcpyAsync(ws + o_wav, hw, hw_words * 4, hipMemcpyHostToDevice,
+	    hipMemcpyAsync(ws + o_wav, hw, nwaves * 4, hipMemcpyHostToDevice,
 	    (hipStream_t)stream) != hipSuccess ||
 	    hipStreamSynchronize((hipStream_t)stream) != hipSuccess;
 	free(hs);

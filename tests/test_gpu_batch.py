@@ -119,17 +119,11 @@ def test_batch_c5_shape(built):
     assert (st[:, 6] == 16).all()      # 32 x 131072 channel blocks over 131072 lanes, / 2
 
 
-VARIANT_SPREAD, VARIANT_CLUSTER = 0x400000, 0x800000     # xa_gpu.hip batch_order
-
-
-@pytest.mark.parametrize("variant", [0, VARIANT_SPREAD, VARIANT_CLUSTER])
-def test_batch_c4_full_size(built, variant):
+def test_batch_c4_full_size(built):
     """BASELINE config C4 at full size in one launch: 1024 streams, stream i
     with bits (4,6,8)[i%3], channels 1+((i/3)&1), 16,384 eblocks, seeded as
     bench.py seeds them; every stream bit-exact against the oracle (decoded
-    on 8 host threads) and its exit state equal.  Also with the waves dealt
-    into the grid in the two experimental orders (tuning bits 22, 23), where
-    a stream's waves are no longer next to each other in the grid."""
+    on 8 host threads) and its exit state equal."""
     import threading
     torch = require_gpu()
     import bench
@@ -145,7 +139,7 @@ def test_batch_c4_full_size(built, variant):
                         "bits": bits, "channels": ch})
     status = torch.zeros(1024 * bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
-    with bjxa_amd.Batch(streams, stream=sh, variant=variant) as b:
+    with bjxa_amd.Batch(streams, stream=sh) as b:
         b.decode(status.data_ptr(), sh)
         torch.cuda.synchronize()
     st = status.cpu().numpy().view(np.uint32).reshape(1024, -1)
