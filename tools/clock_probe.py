@@ -101,6 +101,7 @@ def main():
         for _ in range(10):
             decode()
         pend.append(("hot", "mhz_before", clock()))
+        torch.cuda.synchronize(dev)     # (the GPU idles for the sync's ~50 us)
         ev, wall = timed_decode()
         pend_ev.append(("hot", ev))
         rec["hot"]["wall"].append(wall)
@@ -123,6 +124,19 @@ def main():
         for m, key, k in pend:
             rec[m][key].append(float(c[k, 0]) / float(c[k, 1]) * 100.0)
         pend = []
+    # the clock through a run of decodes that starts after the pause: probe
+    # after every decode (3 runs of 40, median per position)
+    traj = []
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        time.sleep(args.pause / 1e3)
+        ks = []
+        for _ in range(40):
+            decode()
+            ks.append(clock())      # (40 of the 64 slots: no reuse in a run)
+        torch.cuda.synchronize(dev)
+        c = clk.cpu().numpy().reshape(64, 2)
+        traj.append([float(c[k, 0]) / float(c[k, 1]) * 100.0 for k in ks])
     torch.cuda.synchronize(dev)
     c = clk.cpu().numpy().reshape(64, 2)
     for m, key, k in pend:
@@ -138,6 +152,7 @@ def main():
            "probe_ticks": args.ticks, "rounds": args.rounds, "mix": args.mix}
     for m, r in rec.items():
         out[m] = {k: stats(v) for k, v in r.items() if v}
+    out["trajectory_mhz_after_decode_k"] = [round(sorted(col)[1], 1) for col in zip(*traj)]
     print(json.dumps(out))
 
 

@@ -111,10 +111,14 @@ run(const cfg &c)
 			    FLUSH_BYTES / 16, g_sink);
 		CHECK(hipEventRecord(a, 0));
 #define L(W, N) hipLaunchKernelGGL((kw<W, N>), dim3(WGS), dim3(256), 0, 0, g_out, d, rpw, c.row)
-		if (c.width == 16)
-			c.nt ? L(16, 1) : L(16, 0);
+		if (c.width == 16 && c.nt)
+			L(16, 1);
+		else if (c.width == 16)
+			L(16, 0);
+		else if (c.nt)
+			L(4, 1);
 		else
-			c.nt ? L(4, 1) : L(4, 0);
+			L(4, 0);
 #undef L
 		CHECK(hipEventRecord(b, 0));
 		CHECK(hipEventSynchronize(b));
