@@ -51,6 +51,10 @@ struct xa_dec_args {
 				 * (multiples of XA_CHUNK_Q(ch)); chunk q
 				 * starts at eblock q*C */
 	uint32_t init[2];	/* caller state per channel, p0 | p1 << 16 */
+	const uint32_t *init_dev; /* if not NULL: the entry state is read from
+				 * these status words (XA_ST_STATE_L/R) of
+				 * the decode before, in stream order, instead
+				 * of init (xa_gpu.hip duplex_decode's slabs) */
 	uint32_t pace;		/* K1 waves of a workgroup wait for each other
 				 * every `pace` groups (0 = never) */
 	uint2 *g, *e;		/* per-chunk entry / exit state, as repaired */

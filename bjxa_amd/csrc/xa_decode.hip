@@ -624,7 +624,8 @@ spec_wave2(const xa_dec_args &a, uint8_t *region, const uint32_t wchunk0,
 #pragma unroll
 	for (int c = 0; c < CH; c++) {
 		if (b0 - W <= 0)	/* the stream start: the caller's state */
-			xa_unpack_state(a.init[c], p0[c], p1[c]);
+			xa_unpack_state(a.init_dev != nullptr ?
+			    a.init_dev[XA_ST_STATE_L + c] : a.init[c], p0[c], p1[c]);
 		else
 			p0[c] = p1[c] = 0;
 	}
@@ -1152,6 +1153,7 @@ batch_stream_args(const xa_batch_args &b, uint32_t sid)
 	a.pace = 0;	/* the batch kernel decides per workgroup */
 	a.init[0] = d.init[0];
 	a.init[1] = d.init[1];
+	a.init_dev = nullptr;
 	a.g = b.g + d.cbase;
 	a.e = b.e + d.cbase;
 	a.queue = b.queue;

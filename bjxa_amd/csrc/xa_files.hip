@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "xa_decode.h"
+#include "xa_pool.h"
 #include "xa_gpu.h"
 #include "../../include/bjxa_hip.h"
 
@@ -49,110 +50,9 @@ now_ms(void)
 
 namespace {
 
-/* one contiguous host copy */
-struct piece {
-	uint8_t *to;
-	const uint8_t *from;
-	size_t len;
-};
-
-/*
- * Fixed pool of copy threads.  run() splits a list of pieces into equal
- * byte shares (cutting pieces where needed), one per worker plus the
- * calling thread, and returns when every share is copied.
- */
-class copy_pool {
-public:
-	explicit copy_pool(unsigned n) : n_(n)
-	{
-		for (unsigned i = 0; i < n_; i++)
-			th_.emplace_back([this, i] { work(i + 1); });
-	}
-	~copy_pool()
-	{
-		{
-			std::lock_guard<std::mutex> l(m_);
-			quit_ = true;
-		}
-		cv_.notify_all();
-		for (auto &t : th_)
-			t.join();
-	}
-	void run(const std::vector<piece> &p)
-	{
-		size_t total = 0;
-		for (const piece &x : p)
-			total += x.len;
-		if (total == 0)
-			return;
-		/* small jobs on the calling thread only */
-		if (n_ == 0 || total < ((size_t)4 << 20)) {
-			for (const piece &x : p)
-				memcpy(x.to, x.from, x.len);
-			return;
-		}
-		{
-			std::lock_guard<std::mutex> l(m_);
-			job_ = &p;
-			total_ = total;
-			pending_ = n_;
-			gen_++;
-		}
-		cv_.notify_all();
-		share(p, total, 0);
-		std::unique_lock<std::mutex> l(m_);
-		done_.wait(l, [this] { return pending_ == 0; });
-		job_ = NULL;
-	}
-
-private:
-	/* copy bytes [k*total/(n+1), (k+1)*total/(n+1)) of the piece list */
-	void share(const std::vector<piece> &p, size_t total, unsigned k)
-	{
-		const size_t lo = total / (n_ + 1) * k;
-		const size_t hi = k == n_ ? total : total / (n_ + 1) * (k + 1);
-		size_t at = 0;
-		for (const piece &x : p) {
-			const size_t a = std::max(lo, at), b = std::min(hi,
-			    at + x.len);
-			if (a < b)
-				memcpy(x.to + (a - at), x.from + (a - at), b - a);
-			at += x.len;
-			if (at >= hi)
-				break;
-		}
-	}
-	void work(unsigned k)
-	{
-		unsigned long seen = 0;
-		for (;;) {
-			const std::vector<piece> *p;
-			size_t total;
-			{
-				std::unique_lock<std::mutex> l(m_);
-				cv_.wait(l, [&] { return quit_ || gen_ != seen; });
-				if (quit_)
-					return;
-				seen = gen_;
-				p = job_;
-				total = total_;
-			}
-			share(*p, total, k);
-			std::lock_guard<std::mutex> l(m_);
-			if (--pending_ == 0)
-				done_.notify_one();
-		}
-	}
-	unsigned n_;
-	std::vector<std::thread> th_;
-	std::mutex m_;
-	std::condition_variable cv_, done_;
-	const std::vector<piece> *job_ = NULL;
-	size_t total_ = 0;
-	unsigned pending_ = 0;
-	unsigned long gen_ = 0;
-	bool quit_ = false;
-};
+using xa_pool::piece;
+using xa_pool::copy_pool;
+using xa_pool::pool_threads;
 
 /* slab size of the pinned staging buffers */
 constexpr size_t SLAB = (size_t)64 << 20;
@@ -172,19 +72,6 @@ struct files_ctx {
 };
 
 files_ctx ctx;
-
-unsigned
-pool_threads(void)
-{
-	const char *e = getenv("BJXA_THREADS");
-	if (e != NULL && *e != '\0') {
-		const long v = strtol(e, NULL, 10);
-		return v <= 1 ? 0u : (unsigned)std::min(v - 1, 63L);
-	}
-	/* the callers of a GPU box get a share of its cores: stay small */
-	const unsigned hw = std::thread::hardware_concurrency();
-	return std::min(hw > 1 ? hw - 1 : 0u, 15u);
-}
 
 int
 setup(files_ctx &c)

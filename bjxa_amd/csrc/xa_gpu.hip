@@ -11,10 +11,18 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <stdio.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "xa_decode.h"
 #include "xa_gpu.h"
+#include "xa_pool.h"
 #include "../../include/bjxa_hip.h"
 
 #define DEFAULT_WARMUP	8u	/* eblocks; DESIGN.md §3 */
@@ -288,9 +296,12 @@ bjxa_hip_workspace_init(void *d_ws, size_t ws_len, void *stream)
 	return 0;
 }
 
-extern "C" int
-bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
-    uint32_t *d_status, const bjxa_hip_tuning_t *tune, void *stream)
+/* bjxa_hip_decode_async, with the entry state optionally read on the
+ * device from an earlier decode's status words (init_dev, stream order) */
+static int
+decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
+    uint32_t *d_status, const bjxa_hip_tuning_t *tune, void *stream,
+    const uint32_t *init_dev)
 {
 	struct plan p;
 	if (s == NULL || d_ws == NULL || d_status == NULL || s->d_src == NULL ||
@@ -321,6 +332,7 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 	    ((uint32_t)(uint16_t)s->state[1] << 16);
 	a.init[1] = ((uint32_t)(uint16_t)s->state[2]) |
 	    ((uint32_t)(uint16_t)s->state[3] << 16);
+	a.init_dev = init_dev;
 	if (ws_len < ws_bytes(p.nchunks)) {
 		errno = EINVAL;
 		return -1;
@@ -359,6 +371,13 @@ bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
 		return -1;
 	}
 	return 0;
+}
+
+extern "C" int
+bjxa_hip_decode_async(const bjxa_hip_stream_t *s, void *d_ws, size_t ws_len,
+    uint32_t *d_status, const bjxa_hip_tuning_t *tune, void *stream)
+{
+	return decode_async(s, d_ws, ws_len, d_status, tune, stream, NULL);
 }
 
 extern "C" int
@@ -800,6 +819,12 @@ struct bjxa__gpu {
 	uint32_t	*d_status;
 	bool		ws_stale;	/* a call failed: initialise the
 					 * workspace again before the next */
+	/* the duplex route of large calls (duplex_decode), made on first use */
+	hipStream_t	s_in, s_out, s_dec;
+	uint8_t		*h_stage;	/* pinned: DUPLEX_SLOTS staging slots */
+	uint8_t		*d_stage;	/* its device view */
+	uint32_t	*d_sst;		/* per-slab status words */
+	size_t		sst_cap;	/* in slabs */
 };
 
 static int
@@ -878,6 +903,17 @@ bjxa__gpu_free(struct bjxa__gpu *g)
 	(void)hipFree(g->d_status);
 	if (g->h_small != NULL)
 		(void)hipHostFree(g->h_small);
+	if (g->s_in != NULL) {
+		(void)hipStreamSynchronize(g->s_in);
+		(void)hipStreamSynchronize(g->s_out);
+		(void)hipStreamSynchronize(g->s_dec);
+		(void)hipStreamDestroy(g->s_in);
+		(void)hipStreamDestroy(g->s_out);
+		(void)hipStreamDestroy(g->s_dec);
+	}
+	if (g->h_stage != NULL)
+		(void)hipHostFree(g->h_stage);
+	(void)hipFree(g->d_sst);
 	(void)hipStreamDestroy(g->stream);
 	free(g);
 }
@@ -943,24 +979,56 @@ small_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 	return 0;
 }
 
-extern "C" int
-bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
-    unsigned bits, unsigned ch, int16_t state[4], void *dst,
-    uint64_t dst_bytes, uint32_t *err_cb)
+/*
+ * The state at a failing eblock j (bad channel bad_c) of the PCM in g->d_out:
+ * the decode stops before eblock j, as the reference does; the left channel
+ * of that eblock is already advanced if the right block is the bad one
+ * (src/libbjxa.c:633-643).
+ */
+static int
+err_state(struct bjxa__gpu *g, uint32_t j, uint32_t bad_c, unsigned ch,
+    int16_t state[4])
 {
-	device_scope on(g->device);
-	if (eblocks <= XA_SMALL_MAX)
-		return small_decode(g, src, eblocks, bits, ch, state, dst,
-		    dst_bytes, err_cb);
+	int16_t fr[2][2];	/* frames 30, 31 */
+	if (j > 0) {
+		if (hipMemcpy(fr, (uint8_t *)g->d_out + ((size_t)j * 64u * ch) -
+		    4u * ch, 4u * ch, hipMemcpyDeviceToHost) != hipSuccess)
+			return io_fail();
+		for (unsigned c = 0; c < ch; c++) {
+			state[2 * c] = ch == 2 ? fr[1][c] : ((int16_t *)fr)[1];
+			state[2 * c + 1] = ch == 2 ? fr[0][c] : ((int16_t *)fr)[0];
+		}
+	}
+	if (ch == 2 && bad_c == 1) {
+		if (hipMemcpy(fr, (uint8_t *)g->d_out + ((size_t)(j + 1) * 128u) -
+		    8u, 8u, hipMemcpyDeviceToHost) != hipSuccess)
+			return io_fail();
+		state[0] = fr[1][0];
+		state[1] = fr[0][0];
+	}
+	return 0;
+}
 
-	const size_t ebsz = (size_t)(bits * 4 + 1) * ch;
-	const size_t in_bytes = ebsz * eblocks;
+static void
+exit_state(const uint32_t *st, int16_t state[4])
+{
+	state[0] = (int16_t)(st[XA_ST_STATE_L] & 0xffffu);
+	state[1] = (int16_t)(st[XA_ST_STATE_L] >> 16);
+	state[2] = (int16_t)(st[XA_ST_STATE_R] & 0xffffu);
+	state[3] = (int16_t)(st[XA_ST_STATE_R] >> 16);
+}
+
+/* the codec's device buffers for a call of `eblocks` (inputs, PCM, and a
+ * workspace for decodes of up to `ws_eblocks`), the workspace initialised
+ * when new or left stale by a failed call */
+static int
+call_buffers(struct bjxa__gpu *g, uint32_t eblocks, uint32_t ws_eblocks,
+    unsigned bits, unsigned ch)
+{
+	const size_t in_bytes = (size_t)(bits * 4 + 1) * ch * eblocks;
 	const size_t out_full = (size_t)eblocks * 64u * ch;
-	bjxa_hip_stream_t s;
-	uint32_t st[BJXA_HIP_STATUS_WORDS];
 	int fresh = g->d_ws == NULL || g->ws_stale;
-
-	size_t wsn = bjxa_hip_decode_workspace(eblocks, ch, NULL);
+	const size_t wsn = bjxa_hip_decode_workspace(ws_eblocks, ch, NULL);
 	if (grow(&g->d_in, &g->in_cap, in_bytes + 16) < 0 ||
 	    grow(&g->d_out, &g->out_cap, out_full) < 0)
 		return -1;
@@ -970,6 +1038,411 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 		fresh = 1;
 	}
 	if (fresh && bjxa_hip_workspace_init(g->d_ws, g->ws_cap, g->stream) < 0)
+		return -1;
+	return 0;
+}
+
+/*
+ * ------------------------------------------------------------------
+ * Large host-pointer calls with both PCIe directions busy at once
+ * (DESIGN.md §5 R6-7).  The copy engines do not overlap an H2D with a D2H
+ * (the 2M-eblock stereo call's two copies take 6.8 ms together, their
+ * sum), but a kernel's stores into pinned host memory do run beside a copy
+ * engine's H2D (256 MB of kernel stores beside 132 MB of H2D: 4.95 ms;
+ * profiles/r06_zc_duplex.json).  So such a call runs in slabs of
+ * DUPLEX_SLAB PCM bytes:
+ *
+ *   input thread   H2D of slab k's XA from the caller's buffer, registered
+ *                  for the call (copy engine)
+ *   g->s_dec       decode slab k (K1 + tail); its entry state is read on
+ *                  the device from slab k-1's status words
+ *   g->s_out       a copy kernel stores slab k's PCM and status into a
+ *                  pinned staging slot, on CUs of its own (its stores wait
+ *                  on PCIe and would hold up a decode sharing their CUs)
+ *   calling thread and the copy pool: slot -> the caller's dst
+ *
+ * A slot is reused once its host copy is done.  A slab whose status
+ * reports a failing block ends the copies at that eblock, as the serial
+ * route does; nothing is written to dst past it.  BJXA_DUPLEX=0 (read at
+ * the first call) keeps every call on the serial route.
+ */
+#define DUPLEX_SLAB		((size_t)16 << 20)	/* PCM bytes per slab */
+#define DUPLEX_SLOTS		4
+#define DUPLEX_HDR		4096			/* status, then the slab */
+#define DUPLEX_MIN_SLABS	4
+#define DUPLEX_OUT_CUS		64	/* the copy-out stream's CUs; 2 workgroups each */
+
+/*
+ * Slab copy-out, HBM -> pinned host memory.  On CDNA one counter (vmcnt)
+ * covers loads and stores, so waiting for a load also waits for every
+ * store issued before it -- here a store across PCIe.  Each thread loads
+ * SLAB_OUT_U pieces before it stores any, so a wave waits for its stores'
+ * round trip once per SLAB_OUT_U KiB instead of once per KiB.
+ */
+#define SLAB_OUT_U	8
+
+__global__ __launch_bounds__(256) void
+xa_slab_out(const uint4 *src, uint4 *dst, uint64_t n16, const uint32_t *st,
+    uint32_t *st_out)
+{
+	if (blockIdx.x == 0 && threadIdx.x < XA_ST_WORDS)
+		st_out[threadIdx.x] = st[threadIdx.x];
+	const uint64_t step = (uint64_t)gridDim.x * 256u * SLAB_OUT_U;
+	uint64_t i = blockIdx.x * 256ull * SLAB_OUT_U + threadIdx.x;
+	for (; i + 256u * (SLAB_OUT_U - 1) < n16; i += step) {
+		uint4 v[SLAB_OUT_U];
+#pragma unroll
+		for (int u = 0; u < SLAB_OUT_U; u++)
+			v[u] = src[i + 256u * u];
+#pragma unroll
+		for (int u = 0; u < SLAB_OUT_U; u++)
+			dst[i + 256u * u] = v[u];
+	}
+	for (int u = 0; u < SLAB_OUT_U; u++)	/* the last, partial tile */
+		if (i + 256u * u < n16)
+			dst[i + 256u * u] = src[i + 256u * u];
+}
+
+static bool
+duplex_enabled(void)
+{
+	static std::once_flag once;
+	static bool on;
+	std::call_once(once, [] {
+		const char *e = getenv("BJXA_DUPLEX");
+		on = e == NULL || strcmp(e, "0") != 0;
+	});
+	return on;
+}
+
+static std::mutex duplex_pool_mu;
+static xa_pool::copy_pool *duplex_pool;
+
+/* the copy pool of the duplex route (process-wide, one job at a time) */
+static void
+duplex_copy(uint8_t *to, const uint8_t *from, size_t len)
+{
+	std::lock_guard<std::mutex> lk(duplex_pool_mu);
+	if (duplex_pool == NULL)
+		duplex_pool = new xa_pool::copy_pool(xa_pool::pool_threads());
+	std::vector<xa_pool::piece> p(1, xa_pool::piece{ to, from, len });
+	duplex_pool->run(p);
+}
+
+static int
+duplex_setup(struct bjxa__gpu *g, size_t nslab)
+{
+	if (g->s_in == NULL) {
+		/*
+		 * The copy-out kernel's stores go over PCIe and back up every
+		 * CU's memory pipeline they run on, so a decode kernel sharing
+		 * those CUs waits for them (the two serialise, R6-7): the
+		 * copy-out stream and the duplex decode stream get disjoint CU
+		 * masks.
+		 */
+		int ncu = 0;
+		if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount,
+		    g->device) != hipSuccess || ncu <= 0)
+			ncu = 256;
+		const unsigned oc = DUPLEX_OUT_CUS;
+		std::vector<uint32_t> mo((ncu + 31) / 32, 0u), md((ncu + 31) / 32, 0u);
+		const unsigned step = oc > 0 && oc < (unsigned)ncu ? ncu / oc : 1u;
+		for (int c = 0; c < ncu; c++) {
+			const bool out = oc == 0 || (c % step == 0 &&
+			    (unsigned)(c / step) < oc);
+			(out ? mo : md)[c / 32] |= 1u << (c % 32);
+		}
+		bool ok = hipStreamCreateWithFlags(&g->s_in, hipStreamNonBlocking) ==
+		    hipSuccess;
+		if (oc == 0 || oc >= (unsigned)ncu) {
+			ok = ok && hipStreamCreateWithFlags(&g->s_out,
+			    hipStreamNonBlocking) == hipSuccess &&
+			    hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) ==
+			    hipSuccess;
+		} else {
+			ok = ok && hipExtStreamCreateWithCUMask(&g->s_out,
+			    (uint32_t)mo.size(), mo.data()) == hipSuccess &&
+			    hipExtStreamCreateWithCUMask(&g->s_dec, (uint32_t)md.size(),
+			    md.data()) == hipSuccess;
+		}
+		if (!ok) {
+			(void)hipGetLastError();
+			if (g->s_in != NULL)
+				(void)hipStreamDestroy(g->s_in);
+			if (g->s_out != NULL)
+				(void)hipStreamDestroy(g->s_out);
+			if (g->s_dec != NULL)
+				(void)hipStreamDestroy(g->s_dec);
+			g->s_in = g->s_out = g->s_dec = NULL;
+			return io_fail();
+		}
+	}
+	if (g->h_stage == NULL) {
+		if (hipHostMalloc((void **)&g->h_stage, DUPLEX_SLOTS *
+		    (DUPLEX_HDR + DUPLEX_SLAB), hipHostMallocDefault) != hipSuccess) {
+			g->h_stage = NULL;
+			errno = ENOMEM;
+			return -1;
+		}
+		if (hipHostGetDevicePointer((void **)&g->d_stage, g->h_stage, 0) !=
+		    hipSuccess) {
+			(void)hipHostFree(g->h_stage);
+			g->h_stage = NULL;
+			return io_fail();
+		}
+	}
+	if (g->sst_cap < nslab) {
+		(void)hipFree(g->d_sst);
+		g->d_sst = NULL;
+		g->sst_cap = 0;
+		if (hipMalloc((void **)&g->d_sst, nslab * XA_ST_WORDS * 4) !=
+		    hipSuccess) {
+			g->d_sst = NULL;
+			errno = ENOMEM;
+			return -1;
+		}
+		g->sst_cap = nslab;
+	}
+	return 0;
+}
+
+namespace {
+
+/* hipEvents of one duplex call */
+struct event_set {
+	std::vector<hipEvent_t> ev;
+	bool ok = true;
+	explicit event_set(size_t n) : ev(n, NULL)
+	{
+		for (hipEvent_t &e : ev)
+			ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) ==
+			    hipSuccess;
+	}
+	~event_set()
+	{
+		for (hipEvent_t e : ev)
+			if (e != NULL)
+				(void)hipEventDestroy(e);
+	}
+};
+
+/* the input thread's progress: slabs whose H2D is enqueued and its event
+ * recorded */
+struct in_progress {
+	std::mutex m;
+	std::condition_variable cv;
+	size_t ready = 0;
+	bool done = false, failed = false, stop = false;
+};
+
+}	/* namespace */
+
+/* BJXA_DUPLEX_TRACE=1: per-slab host timestamps on stderr (diagnostic) */
+static double
+trace_ms(void)
+{
+	return std::chrono::duration<double, std::milli>(
+	    std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static bool
+duplex_trace(void)
+{
+	static std::once_flag once;
+	static bool on;
+	std::call_once(once, [] { on = getenv("BJXA_DUPLEX_TRACE") != NULL; });
+	return on;
+}
+
+static int
+duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
+    unsigned bits, unsigned ch, int16_t state[4], uint8_t *dst,
+    uint64_t dst_bytes, uint32_t *err_cb)
+{
+	const size_t ebsz = (size_t)(bits * 4 + 1) * ch, ob = 64u * ch;
+	const uint32_t se = (uint32_t)(DUPLEX_SLAB / ob);	/* eblocks per slab */
+	const size_t n = (eblocks + (size_t)se - 1) / se;
+	if (duplex_setup(g, n) < 0 || call_buffers(g, eblocks, se, bits, ch) < 0)
+		return -1;
+	/* (a workspace initialised on g->stream, used on g->s_dec) */
+	if (hipStreamSynchronize(g->stream) != hipSuccess)
+		return io_fail();
+	event_set evs(3 * n);	/* in, decoded, out */
+	if (!evs.ok)
+		return io_fail();
+	hipEvent_t *ev_in = evs.ev.data(), *ev_dec = ev_in + n, *ev_out = ev_dec + n;
+	g->ws_stale = true;	/* cleared when the call completes */
+
+	const bool tr = duplex_trace();
+	std::vector<double> t_in(n, 0.0), t_iss(n, 0.0), t_out(n, 0.0), t_cp(n, 0.0);
+	const double t0 = tr ? trace_ms() : 0.0;
+	in_progress ip;
+	const int dev = g->device;
+	uint8_t *d_in = (uint8_t *)g->d_in;
+	hipStream_t s_in = g->s_in;
+	/* the caller's input registered for the call, so that each slab's H2D
+	 * is a true asynchronous copy at the link rate (from pageable memory
+	 * the runtime's staged copies of 8 MiB ran at ~22 GB/s and paced the
+	 * whole call); where registration fails (memory already pinned or
+	 * registered, say) the copies stay pageable */
+	void *reg_base = NULL;
+	{
+		const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095;
+		const uintptr_t b = ((uintptr_t)src + (size_t)eblocks * ebsz + 4095) &
+		    ~(uintptr_t)4095;
+		if (hipHostRegister((void *)a, b - a, hipHostRegisterDefault) ==
+		    hipSuccess)
+			reg_base = (void *)a;
+		else
+			(void)hipGetLastError();
+	}
+	if (tr)
+		fprintf(stderr, "duplex: register %.3f ms\n", trace_ms() - t0);
+	std::thread input([&, dev, d_in, s_in] {
+		device_scope on(dev);
+		for (size_t k = 0; k < n; k++) {
+			{
+				std::lock_guard<std::mutex> l(ip.m);
+				if (ip.stop)
+					break;
+			}
+			const size_t lo = k * se * ebsz;
+			const size_t len = (std::min((size_t)eblocks, (k + 1) * se) -
+			    k * se) * ebsz;
+			const bool ok = hipMemcpyAsync(d_in + lo, src + lo, len,
+			    hipMemcpyHostToDevice, s_in) == hipSuccess &&
+			    hipEventRecord(ev_in[k], s_in) == hipSuccess;
+			if (tr)
+				t_in[k] = trace_ms() - t0;
+			std::lock_guard<std::mutex> l(ip.m);
+			if (!ok) {
+				ip.failed = true;
+				break;
+			}
+			ip.ready = k + 1;
+			ip.cv.notify_all();
+		}
+		std::lock_guard<std::mutex> l(ip.m);
+		ip.done = true;
+		ip.cv.notify_all();
+	});
+
+	/* enqueue slab k: wait for its input, decode, copy out to its slot */
+	auto issue = [&](size_t k) -> bool {
+		{
+			std::unique_lock<std::mutex> l(ip.m);
+			ip.cv.wait(l, [&] { return ip.ready > k || ip.done; });
+			if (ip.ready <= k)
+				return false;
+		}
+		const uint32_t e0 = (uint32_t)(k * se);
+		const uint32_t ek = std::min(eblocks - e0, se);
+		bjxa_hip_stream_t s;
+		memset(&s, 0, sizeof s);
+		s.d_src = d_in + (size_t)e0 * ebsz;
+		s.d_dst = (uint8_t *)g->d_out + (size_t)e0 * ob;
+		s.eblocks = ek;
+		s.frames = (uint64_t)ek * 32u;
+		s.bits = (uint8_t)bits;
+		s.channels = (uint8_t)ch;
+		memcpy(s.state, state, sizeof s.state);
+		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
+		uint8_t *slot = g->d_stage + (k % DUPLEX_SLOTS) *
+		    (DUPLEX_HDR + DUPLEX_SLAB);
+		if (hipStreamWaitEvent(g->s_dec, ev_in[k], 0) != hipSuccess ||
+		    decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, g->s_dec,
+		    k > 0 ? sst - XA_ST_WORDS : NULL) < 0 ||
+		    hipEventRecord(ev_dec[k], g->s_dec) != hipSuccess ||
+		    hipStreamWaitEvent(g->s_out, ev_dec[k], 0) != hipSuccess)
+			return false;
+		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256), 0,
+		    g->s_out, (const uint4 *)s.d_dst, (uint4 *)(slot + DUPLEX_HDR),
+		    (uint64_t)ek * ob / 16u, sst, (uint32_t *)slot);
+		if (tr)
+			t_iss[k] = trace_ms() - t0;
+		return hipGetLastError() == hipSuccess &&
+		    hipEventRecord(ev_out[k], g->s_out) == hipSuccess;
+	};
+
+	bool ok = true;
+	uint32_t err = 0xffffffffu, fin[XA_ST_WORDS] = { 0 };
+	for (size_t k = 0; ok && k < std::min(n, (size_t)DUPLEX_SLOTS); k++)
+		ok = issue(k);
+	for (size_t k = 0; ok && k < n; k++) {
+		if (hipEventSynchronize(ev_out[k]) != hipSuccess) {
+			ok = false;
+			break;
+		}
+		if (tr)
+			t_out[k] = trace_ms() - t0;
+		const uint8_t *slot = g->h_stage + (k % DUPLEX_SLOTS) *
+		    (DUPLEX_HDR + DUPLEX_SLAB);
+		uint32_t st[XA_ST_WORDS];
+		memcpy(st, (const void *)slot, sizeof st);
+		const size_t lo = k * se * ob;
+		size_t hi = std::min((size_t)dst_bytes, std::min((size_t)eblocks,
+		    (k + 1) * se) * ob);
+		if (st[XA_ST_ERR] != 0xffffffffu) {
+			err = (uint32_t)(k * se * ch) + st[XA_ST_ERR];
+			hi = std::min(hi, (size_t)(err / ch) * ob);
+		}
+		if (hi > lo)
+			duplex_copy(dst + lo, slot + DUPLEX_HDR, hi - lo);
+		if (tr)
+			t_cp[k] = trace_ms() - t0;
+		if (err != 0xffffffffu)
+			break;
+		memcpy(fin, st, sizeof fin);
+		if (k + DUPLEX_SLOTS < n)
+			ok = issue(k + DUPLEX_SLOTS);
+	}
+	{
+		std::lock_guard<std::mutex> l(ip.m);
+		ip.stop = true;
+	}
+	input.join();
+	ok = ok && !ip.failed;
+	if (reg_base != NULL) {
+		(void)hipStreamSynchronize(g->s_in);
+		(void)hipHostUnregister(reg_base);
+	}
+	/* everything enqueued has to finish before the buffers are reused */
+	if (hipStreamSynchronize(g->s_in) != hipSuccess ||
+	    hipStreamSynchronize(g->s_dec) != hipSuccess ||
+	    hipStreamSynchronize(g->s_out) != hipSuccess || !ok)
+		return io_fail();
+	g->ws_stale = false;
+	if (tr) {
+		fprintf(stderr, "duplex %zu slabs, done %.3f ms\n", n, trace_ms() - t0);
+		for (size_t k = 0; k < n; k++)
+			fprintf(stderr, "  slab %2zu in %.3f issued %.3f out %.3f copied %.3f\n",
+			    k, t_in[k], t_iss[k], t_out[k], t_cp[k]);
+	}
+	*err_cb = err;
+	if (err != 0xffffffffu)
+		return err_state(g, err / ch, err % ch, ch, state);
+	exit_state(fin, state);
+	return 0;
+}
+
+extern "C" int
+bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
+    unsigned bits, unsigned ch, int16_t state[4], void *dst,
+    uint64_t dst_bytes, uint32_t *err_cb)
+{
+	device_scope on(g->device);
+	if (eblocks <= XA_SMALL_MAX)
+		return small_decode(g, src, eblocks, bits, ch, state, dst,
+		    dst_bytes, err_cb);
+	if (duplex_enabled() && (uint64_t)eblocks * 64u * ch >=
+	    DUPLEX_MIN_SLABS * DUPLEX_SLAB)
+		return duplex_decode(g, (const uint8_t *)src, eblocks, bits, ch,
+		    state, (uint8_t *)dst, dst_bytes, err_cb);
+
+	const size_t in_bytes = (size_t)(bits * 4 + 1) * ch * eblocks;
+	bjxa_hip_stream_t s;
+	uint32_t st[BJXA_HIP_STATUS_WORDS];
+	if (call_buffers(g, eblocks, eblocks, bits, ch) < 0)
 		return -1;
 	/* cleared once the status of this call has come back */
 	g->ws_stale = true;
@@ -993,35 +1466,13 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 	g->ws_stale = false;
 	*err_cb = st[XA_ST_ERR];
 	if (st[XA_ST_ERR] != 0xffffffffu) {
-		/* stop before the failing eblock, as the reference does; the
-		 * left channel of that eblock is already advanced if the right
-		 * block is the bad one (src/libbjxa.c:633-643) */
 		const uint32_t j = st[XA_ST_ERR] / ch, bad_c = st[XA_ST_ERR] % ch;
-		int16_t fr[2][2];	/* frames 30, 31 */
 		if (dst_bytes > (size_t)j * 64u * ch)
 			dst_bytes = (size_t)j * 64u * ch;
-		if (j > 0) {
-			if (hipMemcpy(fr, (uint8_t *)g->d_out + ((size_t)j * 64u *
-			    ch) - 4u * ch, 4u * ch, hipMemcpyDeviceToHost) !=
-			    hipSuccess)
-				return io_fail();
-			for (unsigned c = 0; c < ch; c++) {
-				state[2 * c] = ch == 2 ? fr[1][c] : ((int16_t *)fr)[1];
-				state[2 * c + 1] = ch == 2 ? fr[0][c] : ((int16_t *)fr)[0];
-			}
-		}
-		if (ch == 2 && bad_c == 1) {
-			if (hipMemcpy(fr, (uint8_t *)g->d_out + ((size_t)(j + 1) *
-			    128u) - 8u, 8u, hipMemcpyDeviceToHost) != hipSuccess)
-				return io_fail();
-			state[0] = fr[1][0];
-			state[1] = fr[0][0];
-		}
+		if (err_state(g, j, bad_c, ch, state) < 0)
+			return -1;
 	} else {
-		state[0] = (int16_t)(st[XA_ST_STATE_L] & 0xffffu);
-		state[1] = (int16_t)(st[XA_ST_STATE_L] >> 16);
-		state[2] = (int16_t)(st[XA_ST_STATE_R] & 0xffffu);
-		state[3] = (int16_t)(st[XA_ST_STATE_R] >> 16);
+		exit_state(st, state);
 	}
 	if (dst_bytes > 0 && hipMemcpy(dst, g->d_out, dst_bytes,
 	    hipMemcpyDeviceToHost) != hipSuccess)

@@ -1,0 +1,141 @@
+"""The duplex route of large host-pointer calls (xa_gpu.hip duplex_decode):
+bjxa_decode() on the caller's host buffers in slabs of 16 MiB of PCM, the
+input on a copy engine while a kernel streams each decoded slab into pinned
+staging and host threads copy it out, each slab's entry state read on the
+device from the slab before.  Through the unchanged host API
+(src/libbjxa.c:602-661, the reference's single-pass caller
+src/bjxa_decode.c:56-100) against the oracle: every format, ragged last
+slabs, cut last blocks, header entry states, a call chained after another,
+and the EPROTO semantics of test/test_decode_error.sh:221-282 with the bad
+block in a middle slab; BJXA_DUPLEX=0 (the serial route) gives the same
+bytes."""
+import errno
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import bjxa_amd
+import oracle
+from bjxa_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+SLAB = 16 << 20             # xa_gpu.hip DUPLEX_SLAB (PCM bytes)
+
+
+def slab_eblocks(ch):
+    return SLAB // (64 * ch)
+
+
+def host_decode(xa, eb, bits, ch, frames, state=(0, 0, 0, 0), fill=0x5A):
+    hdr = bjxa_amd.xa_header(xa.size, frames, 44100, bits, ch, state)
+    dst = np.full(eb * 64 * ch, fill, np.uint8)
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(hdr)
+        assert d.decode(dst, xa) == eb
+    return dst
+
+
+@pytest.mark.parametrize("bits,ch", [(8, 2), (4, 2), (6, 1), (8, 1)])
+def test_duplex_matches_oracle(built, bits, ch):
+    """Five slabs and a ragged sixth, the last block cut, a header state."""
+    eb = 5 * slab_eblocks(ch) + 12_345
+    frames = eb * 32 - 7
+    state = (1234, -4321, -32768, 32767)
+    xa = synth.stream(eb, bits, ch, "A", seed=40 + bits + ch)
+    ref, _, _, _ = oracle.decode(xa, eb, bits, ch, state, frames)
+    dst = host_decode(xa, eb, bits, ch, frames, state)
+    n = frames * ch
+    assert np.array_equal(dst[:2 * n].view(np.int16), ref)
+    assert (dst[2 * n:] == 0x5A).all()          # nothing past the frames
+
+
+def test_duplex_worst_case_mix(built):
+    """Mix W (slowest resync) across slab boundaries: every slab's entry
+    state comes from the slab before, so a wrong hand-off shows at once."""
+    eb = 4 * slab_eblocks(2) + 1
+    xa = synth.stream(eb, 8, 2, "W", seed=41)
+    ref, _, _, _ = oracle.decode(xa, eb, 8, 2)
+    dst = host_decode(xa, eb, 8, 2, eb * 32)
+    assert np.array_equal(dst.view(np.int16), ref)
+
+
+def test_duplex_chained_call(built):
+    """A small call then a large one through one decoder: the large call
+    starts from the state the first left (its slab 0 entry state)."""
+    bits, ch = 8, 2
+    eb0, eb1 = 1000, 4 * slab_eblocks(ch) + 77
+    eb = eb0 + eb1
+    xa = synth.stream(eb, bits, ch, "A", seed=42)
+    ref, _, _, _ = oracle.decode(xa, eb, bits, ch)
+    bx = (bits * 4 + 1) * ch
+    hdr = bjxa_amd.xa_header(xa.size, eb * 32, 44100, bits, ch)
+    out = np.zeros(eb * 64 * ch, np.uint8)
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(hdr)
+        assert d.decode(out[:eb0 * 64 * ch], xa[:eb0 * bx].copy()) == eb0
+        assert d.decode(out[eb0 * 64 * ch:], xa[eb0 * bx:].copy()) == eb1
+    assert np.array_equal(out.view(np.int16), ref)
+
+
+@pytest.mark.parametrize("ch,bad", [(2, 0), (2, 1), (1, 0)])
+def test_duplex_invalid_profile_mid_slab(built, ch, bad):
+    """A gain nibble >= 5 inside slab 2: EPROTO, the eblocks before it in
+    dst and nothing after it, and the carried state the reference's partial
+    update (continuing with the block fixed equals the oracle)."""
+    bits = 8
+    eb = 5 * slab_eblocks(ch) + 100
+    j = 2 * slab_eblocks(ch) + 4567
+    bx = (bits * 4 + 1) * ch
+    xa = synth.stream(eb, bits, ch, "A", seed=43 + ch + bad).reshape(eb * ch, 33)
+    xa[j * ch + bad, 0] = 0x5F
+    hdr = bjxa_amd.xa_header(xa.size, eb * 32, 44100, bits, ch)
+    ref, st_ref, done, badc = oracle.decode(xa.reshape(-1), eb, bits, ch)
+    assert done == j and badc == bad
+    fixed = xa.copy()
+    fixed[j * ch + bad, 0] = 0x00
+    ref2, _, _, _ = oracle.decode(fixed.reshape(-1)[j * bx:], eb - j, bits, ch, st_ref)
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(hdr)
+        dst = np.full(eb * 64 * ch, 0x11, np.uint8)
+        with pytest.raises(bjxa_amd.BjxaError) as ei:
+            d.decode(dst, xa.reshape(-1).copy())
+        assert ei.value.errno == errno.EPROTO
+        assert np.array_equal(dst[:j * 64 * ch].view(np.int16), ref[:j * 32 * ch])
+        assert (dst[j * 64 * ch:] == 0x11).all()
+        rest = eb - j
+        dst2 = np.zeros(rest * 64 * ch, np.uint8)
+        assert d.decode(dst2, fixed.reshape(-1)[j * bx:].copy()) == rest
+        assert np.array_equal(dst2.view(np.int16), ref2)
+
+
+def test_duplex_off_same_bytes(built, tmp_path):
+    """BJXA_DUPLEX=0 (read once per process: a child process) decodes the
+    same stream on the serial route to the same bytes."""
+    eb = 4 * slab_eblocks(2) + 999
+    xa = synth.stream(eb, 8, 2, "A", seed=44)
+    np.save(tmp_path / "xa.npy", xa)
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r)\n"
+        "import bjxa_amd\n"
+        "xa = np.load(%r)\n"
+        "eb = %d\n"
+        "hdr = bjxa_amd.xa_header(xa.size, eb * 32, 44100, 8, 2)\n"
+        "dst = np.zeros(eb * 128, np.uint8)\n"
+        "with bjxa_amd.offload(0), bjxa_amd.Decoder() as d:\n"
+        "    d.parse_header(hdr)\n"
+        "    assert d.decode(dst, xa) == eb\n"
+        "np.save(%r, dst)\n" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                               str(tmp_path / "xa.npy"), eb, str(tmp_path / "off.npy")))
+    env = dict(os.environ, BJXA_DUPLEX="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    off = np.load(tmp_path / "off.npy")
+    on = host_decode(xa, eb, 8, 2, eb * 32)
+    assert np.array_equal(on, off)
+    ref, _, _, _ = oracle.decode(xa, eb, 8, 2)
+    assert np.array_equal(on.view(np.int16), ref)
