@@ -1254,50 +1254,51 @@ duplex_trace(void)
 	return on;
 }
 
+/*
+ * One duplex call over n slabs (decode or encode).  The caller's input
+ * (in_bytes at src) is registered for the call, so that each slab's H2D is
+ * a true asynchronous copy at the link rate (from pageable memory the
+ * runtime's staged copies of 8 MiB ran at ~22 GB/s and paced the whole
+ * call); where registration fails (memory already pinned or registered,
+ * say) the copies stay pageable.
+ *   in_range(k, &off, &len)    slab k's input bytes [off, off + len)
+ *   gpu(k, slot)               enqueue slab k's kernel on g->s_dec (after
+ *                              ev_in[k]) and its copy-out into the device
+ *                              view of staging slot `slot` on g->s_out;
+ *                              false on failure
+ *   host(k, slot)              the calling thread's part once slab k is in
+ *                              its slot: copy it out; returns 1 to go on,
+ *                              0 to stop early (an error the caller
+ *                              reports), -1 on failure
+ * Returns 0 or -1/errno; every enqueued operation has finished on return.
+ */
+template <class InRange, class Gpu, class Host>
 static int
-duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
-    unsigned bits, unsigned ch, int16_t state[4], uint8_t *dst,
-    uint64_t dst_bytes, uint32_t *err_cb)
+duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
+    InRange &&in_range, Gpu &&gpu, Host &&host)
 {
-	const size_t ebsz = (size_t)(bits * 4 + 1) * ch, ob = 64u * ch;
-	const uint32_t se = (uint32_t)(DUPLEX_SLAB / ob);	/* eblocks per slab */
-	const size_t n = (eblocks + (size_t)se - 1) / se;
-	if (duplex_setup(g, n) < 0 || call_buffers(g, eblocks, se, bits, ch) < 0)
-		return -1;
-	/* (a workspace initialised on g->stream, used on g->s_dec) */
-	if (hipStreamSynchronize(g->stream) != hipSuccess)
-		return io_fail();
-	event_set evs(3 * n);	/* in, decoded, out */
+	event_set evs(3 * n);	/* in, kernel done, out */
 	if (!evs.ok)
 		return io_fail();
 	hipEvent_t *ev_in = evs.ev.data(), *ev_dec = ev_in + n, *ev_out = ev_dec + n;
-	g->ws_stale = true;	/* cleared when the call completes */
-
 	const bool tr = duplex_trace();
 	std::vector<double> t_in(n, 0.0), t_iss(n, 0.0), t_out(n, 0.0), t_cp(n, 0.0);
 	const double t0 = tr ? trace_ms() : 0.0;
-	in_progress ip;
-	const int dev = g->device;
-	uint8_t *d_in = (uint8_t *)g->d_in;
-	hipStream_t s_in = g->s_in;
-	/* the caller's input registered for the call, so that each slab's H2D
-	 * is a true asynchronous copy at the link rate (from pageable memory
-	 * the runtime's staged copies of 8 MiB ran at ~22 GB/s and paced the
-	 * whole call); where registration fails (memory already pinned or
-	 * registered, say) the copies stay pageable */
+
 	void *reg_base = NULL;
 	{
 		const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095;
-		const uintptr_t b = ((uintptr_t)src + (size_t)eblocks * ebsz + 4095) &
-		    ~(uintptr_t)4095;
+		const uintptr_t b = ((uintptr_t)src + in_bytes + 4095) & ~(uintptr_t)4095;
 		if (hipHostRegister((void *)a, b - a, hipHostRegisterDefault) ==
 		    hipSuccess)
 			reg_base = (void *)a;
 		else
 			(void)hipGetLastError();
 	}
-	if (tr)
-		fprintf(stderr, "duplex: register %.3f ms\n", trace_ms() - t0);
+	in_progress ip;
+	const int dev = g->device;
+	uint8_t *d_in = (uint8_t *)g->d_in;
+	hipStream_t s_in = g->s_in;
 	std::thread input([&, dev, d_in, s_in] {
 		device_scope on(dev);
 		for (size_t k = 0; k < n; k++) {
@@ -1306,10 +1307,9 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 				if (ip.stop)
 					break;
 			}
-			const size_t lo = k * se * ebsz;
-			const size_t len = (std::min((size_t)eblocks, (k + 1) * se) -
-			    k * se) * ebsz;
-			const bool ok = hipMemcpyAsync(d_in + lo, src + lo, len,
+			size_t off, len;
+			in_range(k, &off, &len);
+			const bool ok = hipMemcpyAsync(d_in + off, src + off, len,
 			    hipMemcpyHostToDevice, s_in) == hipSuccess &&
 			    hipEventRecord(ev_in[k], s_in) == hipSuccess;
 			if (tr)
@@ -1327,7 +1327,6 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 		ip.cv.notify_all();
 	});
 
-	/* enqueue slab k: wait for its input, decode, copy out to its slot */
 	auto issue = [&](size_t k) -> bool {
 		{
 			std::unique_lock<std::mutex> l(ip.m);
@@ -1335,37 +1334,18 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 			if (ip.ready <= k)
 				return false;
 		}
-		const uint32_t e0 = (uint32_t)(k * se);
-		const uint32_t ek = std::min(eblocks - e0, se);
-		bjxa_hip_stream_t s;
-		memset(&s, 0, sizeof s);
-		s.d_src = d_in + (size_t)e0 * ebsz;
-		s.d_dst = (uint8_t *)g->d_out + (size_t)e0 * ob;
-		s.eblocks = ek;
-		s.frames = (uint64_t)ek * 32u;
-		s.bits = (uint8_t)bits;
-		s.channels = (uint8_t)ch;
-		memcpy(s.state, state, sizeof s.state);
-		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
 		uint8_t *slot = g->d_stage + (k % DUPLEX_SLOTS) *
 		    (DUPLEX_HDR + DUPLEX_SLAB);
 		if (hipStreamWaitEvent(g->s_dec, ev_in[k], 0) != hipSuccess ||
-		    decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, g->s_dec,
-		    k > 0 ? sst - XA_ST_WORDS : NULL) < 0 ||
-		    hipEventRecord(ev_dec[k], g->s_dec) != hipSuccess ||
-		    hipStreamWaitEvent(g->s_out, ev_dec[k], 0) != hipSuccess)
+		    !gpu(k, slot, ev_dec[k]) ||
+		    hipEventRecord(ev_out[k], g->s_out) != hipSuccess)
 			return false;
-		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256), 0,
-		    g->s_out, (const uint4 *)s.d_dst, (uint4 *)(slot + DUPLEX_HDR),
-		    (uint64_t)ek * ob / 16u, sst, (uint32_t *)slot);
 		if (tr)
 			t_iss[k] = trace_ms() - t0;
-		return hipGetLastError() == hipSuccess &&
-		    hipEventRecord(ev_out[k], g->s_out) == hipSuccess;
+		return true;
 	};
 
 	bool ok = true;
-	uint32_t err = 0xffffffffu, fin[XA_ST_WORDS] = { 0 };
 	for (size_t k = 0; ok && k < std::min(n, (size_t)DUPLEX_SLOTS); k++)
 		ok = issue(k);
 	for (size_t k = 0; ok && k < n; k++) {
@@ -1375,24 +1355,14 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 		}
 		if (tr)
 			t_out[k] = trace_ms() - t0;
-		const uint8_t *slot = g->h_stage + (k % DUPLEX_SLOTS) *
-		    (DUPLEX_HDR + DUPLEX_SLAB);
-		uint32_t st[XA_ST_WORDS];
-		memcpy(st, (const void *)slot, sizeof st);
-		const size_t lo = k * se * ob;
-		size_t hi = std::min((size_t)dst_bytes, std::min((size_t)eblocks,
-		    (k + 1) * se) * ob);
-		if (st[XA_ST_ERR] != 0xffffffffu) {
-			err = (uint32_t)(k * se * ch) + st[XA_ST_ERR];
-			hi = std::min(hi, (size_t)(err / ch) * ob);
-		}
-		if (hi > lo)
-			duplex_copy(dst + lo, slot + DUPLEX_HDR, hi - lo);
+		const int r = host(k, g->h_stage + (k % DUPLEX_SLOTS) *
+		    (DUPLEX_HDR + DUPLEX_SLAB));
 		if (tr)
 			t_cp[k] = trace_ms() - t0;
-		if (err != 0xffffffffu)
+		if (r <= 0) {
+			ok = r == 0;
 			break;
-		memcpy(fin, st, sizeof fin);
+		}
 		if (k + DUPLEX_SLOTS < n)
 			ok = issue(k + DUPLEX_SLOTS);
 	}
@@ -1402,27 +1372,136 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 	}
 	input.join();
 	ok = ok && !ip.failed;
-	if (reg_base != NULL) {
-		(void)hipStreamSynchronize(g->s_in);
-		(void)hipHostUnregister(reg_base);
-	}
 	/* everything enqueued has to finish before the buffers are reused */
-	if (hipStreamSynchronize(g->s_in) != hipSuccess ||
-	    hipStreamSynchronize(g->s_dec) != hipSuccess ||
-	    hipStreamSynchronize(g->s_out) != hipSuccess || !ok)
-		return io_fail();
-	g->ws_stale = false;
+	const bool synced = hipStreamSynchronize(g->s_in) == hipSuccess &&
+	    hipStreamSynchronize(g->s_dec) == hipSuccess &&
+	    hipStreamSynchronize(g->s_out) == hipSuccess;
+	if (reg_base != NULL)
+		(void)hipHostUnregister(reg_base);
 	if (tr) {
 		fprintf(stderr, "duplex %zu slabs, done %.3f ms\n", n, trace_ms() - t0);
 		for (size_t k = 0; k < n; k++)
 			fprintf(stderr, "  slab %2zu in %.3f issued %.3f out %.3f copied %.3f\n",
 			    k, t_in[k], t_iss[k], t_out[k], t_cp[k]);
 	}
+	return synced && ok ? 0 : io_fail();
+}
+
+static int
+duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
+    unsigned bits, unsigned ch, int16_t state[4], uint8_t *dst,
+    uint64_t dst_bytes, uint32_t *err_cb)
+{
+	const size_t ebsz = (size_t)(bits * 4 + 1) * ch, ob = 64u * ch;
+	const uint32_t se = (uint32_t)(DUPLEX_SLAB / ob);	/* eblocks per slab */
+	const size_t n = (eblocks + (size_t)se - 1) / se;
+	if (duplex_setup(g, n) < 0 || call_buffers(g, eblocks, se, bits, ch) < 0)
+		return -1;
+	/* (a workspace initialised on g->stream, used on g->s_dec) */
+	if (hipStreamSynchronize(g->stream) != hipSuccess)
+		return io_fail();
+	g->ws_stale = true;	/* cleared when the call completes */
+	uint32_t err = 0xffffffffu, fin[XA_ST_WORDS] = { 0 };
+	auto slab_eb = [&](size_t k) {
+		return (uint32_t)std::min((size_t)eblocks - k * se, (size_t)se);
+	};
+	const int r = duplex_run(g, n, src, (size_t)eblocks * ebsz,
+	    [&](size_t k, size_t *off, size_t *len) {
+		*off = k * se * ebsz;
+		*len = slab_eb(k) * ebsz;
+	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done) -> bool {
+		const uint32_t e0 = (uint32_t)(k * se), ek = slab_eb(k);
+		bjxa_hip_stream_t s;
+		memset(&s, 0, sizeof s);
+		s.d_src = (uint8_t *)g->d_in + (size_t)e0 * ebsz;
+		s.d_dst = (uint8_t *)g->d_out + (size_t)e0 * ob;
+		s.eblocks = ek;
+		s.frames = (uint64_t)ek * 32u;
+		s.bits = (uint8_t)bits;
+		s.channels = (uint8_t)ch;
+		memcpy(s.state, state, sizeof s.state);
+		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
+		if (decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, g->s_dec,
+		    k > 0 ? sst - XA_ST_WORDS : NULL) < 0 ||
+		    hipEventRecord(ev_done, g->s_dec) != hipSuccess ||
+		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
+			return false;
+		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256),
+		    0, g->s_out, (const uint4 *)s.d_dst, (uint4 *)(slot + DUPLEX_HDR),
+		    (uint64_t)ek * ob / 16u, sst, (uint32_t *)slot);
+		return hipGetLastError() == hipSuccess;
+	}, [&](size_t k, const uint8_t *slot) -> int {
+		uint32_t st[XA_ST_WORDS];
+		memcpy(st, (const void *)slot, sizeof st);
+		const size_t lo = k * se * ob;
+		size_t hi = std::min((size_t)dst_bytes, (k * se + slab_eb(k)) * ob);
+		if (st[XA_ST_ERR] != 0xffffffffu) {
+			err = (uint32_t)(k * se * ch) + st[XA_ST_ERR];
+			hi = std::min(hi, (size_t)(err / ch) * ob);
+		}
+		if (hi > lo)
+			duplex_copy(dst + lo, slot + DUPLEX_HDR, hi - lo);
+		if (err != 0xffffffffu)
+			return 0;
+		memcpy(fin, st, sizeof fin);
+		return 1;
+	});
+	if (r < 0)
+		return -1;
+	g->ws_stale = false;
 	*err_cb = err;
 	if (err != 0xffffffffu)
 		return err_state(g, err / ch, err % ch, ch, state);
 	exit_state(fin, state);
 	return 0;
+}
+
+/*
+ * The same route for a large encode: PCM slabs in on the copy engine (the
+ * long direction, 256 MB for a 2M-eblock stereo call), the encode kernel
+ * per slab, and its XA (132 MB) streamed to pinned staging by the copy
+ * kernel.  Slabs are independent (the encoder keeps no state, :665-691).
+ */
+static int
+duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
+    unsigned bits, unsigned ch, uint8_t *dst)
+{
+	const size_t ebsz = (size_t)(bits * 4 + 1) * ch, ib = 64u * ch;
+	const uint32_t eblocks = (uint32_t)((frames + 31) / 32);
+	const uint32_t se = (uint32_t)(DUPLEX_SLAB / ib);	/* eblocks per slab */
+	const size_t n = (eblocks + (size_t)se - 1) / se;
+	const size_t in_bytes = (size_t)frames * 2u * ch;
+	if (duplex_setup(g, n) < 0 ||
+	    grow(&g->d_in, &g->in_cap, (size_t)eblocks * ib + 256) < 0 ||
+	    grow(&g->d_out, &g->out_cap, (size_t)eblocks * ebsz + 256) < 0)
+		return -1;
+	auto slab_frames = [&](size_t k) {
+		return std::min((uint64_t)frames - (uint64_t)k * se * 32u,
+		    (uint64_t)se * 32u);
+	};
+	return duplex_run(g, n, src, in_bytes,
+	    [&](size_t k, size_t *off, size_t *len) {
+		*off = k * se * ib;
+		*len = (size_t)slab_frames(k) * 2u * ch;
+	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done) -> bool {
+		const uint64_t fk = slab_frames(k);
+		const size_t xk = (size_t)((fk + 31) / 32) * ebsz;
+		uint8_t *d_xa = (uint8_t *)g->d_out + k * se * ebsz;
+		if (bjxa_hip_encode_async((uint8_t *)g->d_in + k * se * ib, fk, bits,
+		    ch, d_xa, g->s_dec) < 0 ||
+		    hipEventRecord(ev_done, g->s_dec) != hipSuccess ||
+		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
+			return false;
+		/* whole 16-B pieces (the slot has room past the slab's XA) */
+		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256),
+		    0, g->s_out, (const uint4 *)d_xa, (uint4 *)(slot + DUPLEX_HDR),
+		    (uint64_t)((xk + 15) / 16), g->d_sst, (uint32_t *)slot);
+		return hipGetLastError() == hipSuccess;
+	}, [&](size_t k, const uint8_t *slot) -> int {
+		const size_t xk = (size_t)((slab_frames(k) + 31) / 32) * ebsz;
+		duplex_copy(dst + k * se * ebsz, slot + DUPLEX_HDR, xk);
+		return 1;
+	});
 }
 
 extern "C" int
@@ -1502,6 +1581,10 @@ bjxa__gpu_encode(struct bjxa__gpu *g, const void *src, uint64_t frames,
 		return 0;
 	}
 
+	if (duplex_enabled() && (uint64_t)eblocks * 64u * ch >=
+	    DUPLEX_MIN_SLABS * DUPLEX_SLAB)
+		return duplex_encode(g, (const uint8_t *)src, frames, bits, ch,
+		    (uint8_t *)dst);
 	if (grow(&g->d_in, &g->in_cap, in_bytes + 256) < 0 ||
 	    grow(&g->d_out, &g->out_cap, out_bytes + 256) < 0)
 		return -1;

@@ -28,7 +28,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ch", type=int, default=2)
     ap.add_argument("--passes", type=int, default=5)
+    ap.add_argument("--encode", action="store_true",
+                    help="bjxa_encode() of the same stream's PCM instead")
     args = ap.parse_args()
+    if args.encode:
+        return encode_rate(args)
     ch = args.ch
     eb = 2_000_000 if ch == 2 else 4_000_000
     bits = 8
@@ -53,6 +57,35 @@ def main():
                       "MSamples_per_s": round(samples / med / 1e6, 1),
                       "host_GB_per_s": round((len(xa) + dst.nbytes) / med / 1e9, 2),
                       "first_call_ms": round(times[0] * 1e3, 3), "bit_exact": ok}))
+
+
+def encode_rate(args):
+    """bjxa_encode() on host buffers: the PCM of the same largest stream
+    (64M stereo / 128M mono frames) into XA, one call."""
+    ch = args.ch
+    eb = 2_000_000 if ch == 2 else 4_000_000
+    bits, frames = 8, eb * 32
+    pcm = synth.pcm(frames, ch, seed=7)
+    fmt0 = {"data_len_pcm": frames * 2 * ch, "blocks": 0, "block_size_pcm": 0,
+            "block_size_xa": 0, "samples_rate": 44100, "sample_bits": 16, "channels": ch}
+    dst = np.zeros(eb * ch * (bits * 4 + 1), np.uint8)
+    times = []
+    e = bjxa_amd.Encoder()         # one codec: device buffers persist
+    for i in range(args.passes + 1):
+        fmt = e.init(fmt0, bits)
+        t = time.perf_counter()
+        n = e.encode(dst, pcm.view(np.uint8))
+        times.append(time.perf_counter() - t)
+        assert n == fmt["blocks"] == eb, n
+    e.close()
+    import oracle
+    ok = bool(np.array_equal(dst, oracle.encode(pcm, frames, bits, ch)))
+    med = float(np.median(times[1:]))
+    print(json.dumps({"api": "bjxa_encode (host buffers)", "bits": bits, "channels": ch,
+                      "eblocks": eb, "ms": round(med * 1e3, 3),
+                      "MSamples_per_s": round(frames * ch / med / 1e6, 1),
+                      "host_GB_per_s": round((pcm.nbytes + dst.nbytes) / med / 1e9, 2),
+                      "first_call_ms": round(times[0] * 1e3, 3), "byte_exact": ok}))
 
 
 if __name__ == "__main__":
