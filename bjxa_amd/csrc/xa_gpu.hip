@@ -1103,35 +1103,6 @@ xa_slab_out(const uint4 *src, uint4 *dst, uint64_t n16, const uint32_t *st,
 			dst[i + 256u * u] = src[i + 256u * u];
 }
 
-/* host (registered, device-mapped) -> HBM, 16-B pieces */
-__global__ __launch_bounds__(256) void
-xa_slab_in(const uint4 *src, uint4 *dst, uint64_t n16)
-{
-	const uint64_t step = (uint64_t)gridDim.x * 256u * SLAB_OUT_U;
-	uint64_t i = blockIdx.x * 256ull * SLAB_OUT_U + threadIdx.x;
-	for (; i + 256u * (SLAB_OUT_U - 1) < n16; i += step) {
-		uint4 v[SLAB_OUT_U];
-#pragma unroll
-		for (int u = 0; u < SLAB_OUT_U; u++)
-			v[u] = src[i + 256u * u];
-#pragma unroll
-		for (int u = 0; u < SLAB_OUT_U; u++)
-			dst[i + 256u * u] = v[u];
-	}
-	for (int u = 0; u < SLAB_OUT_U; u++)
-		if (i + 256u * u < n16)
-			dst[i + 256u * u] = src[i + 256u * u];
-}
-
-/* diagnostic: BJXA_DUPLEX_KIN=1 moves the input with copy-in kernels
- * reading the registered input instead of the copy engine */
-static bool
-kernel_in(void)
-{
-	static const bool v = getenv("BJXA_DUPLEX_KIN") != NULL;
-	return v;
-}
-
 static bool
 duplex_enabled(void)
 {
@@ -1181,19 +1152,15 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 			    (unsigned)(c / step) < oc);
 			(out ? mo : md)[c / 32] |= 1u << (c % 32);
 		}
-		bool ok = true;
+		bool ok = hipStreamCreateWithFlags(&g->s_in, hipStreamNonBlocking) ==
+		    hipSuccess;
 		if (oc == 0 || oc >= (unsigned)ncu) {
-			ok = hipStreamCreateWithFlags(&g->s_in, hipStreamNonBlocking) ==
-			    hipSuccess && hipStreamCreateWithFlags(&g->s_out,
+			ok = ok && hipStreamCreateWithFlags(&g->s_out,
 			    hipStreamNonBlocking) == hipSuccess &&
 			    hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) ==
 			    hipSuccess;
 		} else {
-			/* (s_in: the copy-in kernels of kernel_in(), with the
-			 * copy-out's CUs) */
-			ok = hipExtStreamCreateWithCUMask(&g->s_in,
-			    (uint32_t)mo.size(), mo.data()) == hipSuccess &&
-			    hipExtStreamCreateWithCUMask(&g->s_out,
+			ok = ok && hipExtStreamCreateWithCUMask(&g->s_out,
 			    (uint32_t)mo.size(), mo.data()) == hipSuccess &&
 			    hipExtStreamCreateWithCUMask(&g->s_dec, (uint32_t)md.size(),
 			    md.data()) == hipSuccess;
@@ -1319,21 +1286,14 @@ duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	const double t0 = tr ? trace_ms() : 0.0;
 
 	void *reg_base = NULL;
-	const uint8_t *src_dev = NULL;	/* device view of the registered input */
 	{
 		const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095;
 		const uintptr_t b = ((uintptr_t)src + in_bytes + 4095) & ~(uintptr_t)4095;
-		if (hipHostRegister((void *)a, b - a, hipHostRegisterMapped) ==
-		    hipSuccess) {
+		if (hipHostRegister((void *)a, b - a, hipHostRegisterDefault) ==
+		    hipSuccess)
 			reg_base = (void *)a;
-			void *dp = NULL;
-			if (kernel_in() && hipHostGetDevicePointer(&dp, reg_base, 0) ==
-			    hipSuccess && ((uintptr_t)src & 15u) == 0)
-				src_dev = (const uint8_t *)dp + ((uintptr_t)src - a);
+		else
 			(void)hipGetLastError();
-		} else {
-			(void)hipGetLastError();
-		}
 	}
 	in_progress ip;
 	const int dev = g->device;
@@ -1349,17 +1309,9 @@ duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 			}
 			size_t off, len;
 			in_range(k, &off, &len);
-			bool ok;
-			if (src_dev != NULL && (off & 15u) == 0) {
-				hipLaunchKernelGGL(xa_slab_in, dim3(2 * DUPLEX_OUT_CUS),
-				    dim3(256), 0, s_in, (const uint4 *)(src_dev + off),
-				    (uint4 *)(d_in + off), (uint64_t)((len + 15) / 16));
-				ok = hipGetLastError() == hipSuccess;
-			} else {
-				ok = hipMemcpyAsync(d_in + off, src + off, len,
-				    hipMemcpyHostToDevice, s_in) == hipSuccess;
-			}
-			ok = ok && hipEventRecord(ev_in[k], s_in) == hipSuccess;
+			const bool ok = hipMemcpyAsync(d_in + off, src + off, len,
+			    hipMemcpyHostToDevice, s_in) == hipSuccess &&
+			    hipEventRecord(ev_in[k], s_in) == hipSuccess;
 			if (tr)
 				t_in[k] = trace_ms() - t0;
 			std::lock_guard<std::mutex> l(ip.m);
