@@ -1123,10 +1123,14 @@ static void
 duplex_copy(uint8_t *to, const uint8_t *from, size_t len)
 {
 	std::lock_guard<std::mutex> lk(duplex_pool_mu);
-	if (duplex_pool == NULL)
-		duplex_pool = new xa_pool::copy_pool(xa_pool::pool_threads());
-	std::vector<xa_pool::piece> p(1, xa_pool::piece{ to, from, len });
-	duplex_pool->run(p);
+	try {
+		if (duplex_pool == NULL)
+			duplex_pool = new xa_pool::copy_pool(xa_pool::pool_threads());
+		std::vector<xa_pool::piece> p(1, xa_pool::piece{ to, from, len });
+		duplex_pool->run(p);
+	} catch (...) {
+		memcpy(to, from, len);	/* no memory for the pool: copy here */
+	}
 }
 
 static int
@@ -1274,7 +1278,27 @@ duplex_trace(void)
  */
 template <class InRange, class Gpu, class Host>
 static int
+duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
+    InRange &&in_range, Gpu &&gpu, Host &&host);
+
+/* (the C ABI lets no exception out: allocations and the input thread may
+ * fail before anything is enqueued, and nothing after that throws) */
+template <class InRange, class Gpu, class Host>
+static int
 duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
+    InRange &&in_range, Gpu &&gpu, Host &&host)
+{
+	try {
+		return duplex_run_(g, n, src, in_bytes, in_range, gpu, host);
+	} catch (...) {
+		errno = ENOMEM;
+		return -1;
+	}
+}
+
+template <class InRange, class Gpu, class Host>
+static int
+duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
     InRange &&in_range, Gpu &&gpu, Host &&host)
 {
 	event_set evs(3 * n);	/* in, kernel done, out */
@@ -1299,7 +1323,7 @@ duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	const int dev = g->device;
 	uint8_t *d_in = (uint8_t *)g->d_in;
 	hipStream_t s_in = g->s_in;
-	std::thread input([&, dev, d_in, s_in] {
+	auto input_body = [&, dev, d_in, s_in] {
 		device_scope on(dev);
 		for (size_t k = 0; k < n; k++) {
 			{
@@ -1325,7 +1349,16 @@ duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 		std::lock_guard<std::mutex> l(ip.m);
 		ip.done = true;
 		ip.cv.notify_all();
-	});
+	};
+	std::thread input;
+	try {
+		input = std::thread(input_body);
+	} catch (...) {
+		if (reg_base != NULL)
+			(void)hipHostUnregister(reg_base);
+		errno = EAGAIN;
+		return -1;
+	}
 
 	auto issue = [&](size_t k) -> bool {
 		{

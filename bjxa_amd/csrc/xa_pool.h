@@ -31,10 +31,18 @@ struct piece {
  */
 class copy_pool {
 public:
-	explicit copy_pool(unsigned n) : n_(n)
+	/* n workers, or as many as could be started (a share per started
+	 * worker; with none the calling thread copies everything) */
+	explicit copy_pool(unsigned n) : n_(0)
 	{
-		for (unsigned i = 0; i < n_; i++)
-			th_.emplace_back([this, i] { work(i + 1); });
+		try {
+			th_.reserve(n);
+			for (unsigned i = 0; i < n; i++) {
+				th_.emplace_back([this, i] { work(i + 1); });
+				n_++;
+			}
+		} catch (...) {
+		}
 	}
 	~copy_pool()
 	{
