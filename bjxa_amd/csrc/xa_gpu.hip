@@ -1163,11 +1163,20 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 			    hipStreamNonBlocking) == hipSuccess &&
 			    hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) ==
 			    hipSuccess;
-		} else {
-			ok = ok && hipExtStreamCreateWithCUMask(&g->s_out,
-			    (uint32_t)mo.size(), mo.data()) == hipSuccess &&
-			    hipExtStreamCreateWithCUMask(&g->s_dec, (uint32_t)md.size(),
-			    md.data()) == hipSuccess;
+		} else if (ok) {
+			if (hipExtStreamCreateWithCUMask(&g->s_out, (uint32_t)mo.size(),
+			    mo.data()) != hipSuccess || hipExtStreamCreateWithCUMask(
+			    &g->s_dec, (uint32_t)md.size(), md.data()) != hipSuccess) {
+				/* no CU masks here: plain streams (slower, R6-7) */
+				(void)hipGetLastError();
+				if (g->s_out != NULL)
+					(void)hipStreamDestroy(g->s_out);
+				g->s_out = NULL;
+				ok = hipStreamCreateWithFlags(&g->s_out,
+				    hipStreamNonBlocking) == hipSuccess &&
+				    (g->s_dec != NULL || hipStreamCreateWithFlags(&g->s_dec,
+				    hipStreamNonBlocking) == hipSuccess);
+			}
 		}
 		if (!ok) {
 			(void)hipGetLastError();
