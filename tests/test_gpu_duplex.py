@@ -164,3 +164,45 @@ def test_duplex_encode_matches_oracle(built, bits, ch):
     pcm = synth.pcm(frames, ch, seed=50 + bits + ch)
     got = host_encode(pcm, frames, bits, ch)
     assert np.array_equal(got, oracle.encode(pcm, frames, bits, ch))
+
+
+def test_duplex_pinned_input(built):
+    """Input already in pinned memory: the route's registration of it
+    fails (it is registered already) and the slabs go in as plain copies;
+    same bytes."""
+    import torch
+    eb = 4 * slab_eblocks(2) + 5
+    xa = synth.stream(eb, 8, 2, "A", seed=45)
+    pinned = torch.empty(xa.size, dtype=torch.uint8, pin_memory=True)
+    pinned.numpy()[:] = xa
+    ref, _, _, _ = oracle.decode(xa, eb, 8, 2)
+    dst = host_decode(pinned.numpy(), eb, 8, 2, eb * 32)
+    assert np.array_equal(dst.view(np.int16), ref)
+
+
+def test_duplex_concurrent_codecs(built):
+    """Two codecs on two threads, each a duplex-sized call at once: each
+    has its own streams, staging and workspace; the host copy pool is
+    shared (one job at a time).  Both bit-exact."""
+    import threading
+    jobs = []
+    for i, (bits, ch) in enumerate([(8, 2), (4, 1)]):
+        eb = 4 * slab_eblocks(ch) + 333 * (i + 1)
+        xa = synth.stream(eb, bits, ch, "A", seed=46 + i)
+        jobs.append((xa, eb, bits, ch, oracle.decode(xa, eb, bits, ch)[0]))
+    out, errs = [None] * len(jobs), []
+
+    def run(i):
+        try:
+            xa, eb, bits, ch, _ = jobs[i]
+            out[i] = host_decode(xa, eb, bits, ch, eb * 32)
+        except Exception as e:      # reported below
+            errs.append(e)
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(jobs))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    for (xa, eb, bits, ch, ref), got in zip(jobs, out):
+        assert np.array_equal(got.view(np.int16), ref)
