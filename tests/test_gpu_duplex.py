@@ -81,14 +81,19 @@ def test_duplex_chained_call(built):
     assert np.array_equal(out.view(np.int16), ref)
 
 
-@pytest.mark.parametrize("ch,bad", [(2, 0), (2, 1), (1, 0)])
-def test_duplex_invalid_profile_mid_slab(built, ch, bad):
-    """A gain nibble >= 5 inside slab 2: EPROTO, the eblocks before it in
-    dst and nothing after it, and the carried state the reference's partial
-    update (continuing with the block fixed equals the oracle)."""
+@pytest.mark.parametrize("ch,bad,where", [(2, 0, "mid"), (2, 1, "mid"), (1, 0, "mid"),
+                                          (2, 1, "first"), (2, 0, "boundary"),
+                                          (1, 0, "boundary"), (2, 1, "last")])
+def test_duplex_invalid_profile_mid_slab(built, ch, bad, where):
+    """A gain nibble >= 5 inside slab 2 (mid), in slab 0 (first), on the
+    first eblock of slab 3 (boundary: slab 2 copied whole, nothing of slab
+    3) or on the stream's last eblock (last): EPROTO, the eblocks before it
+    in dst and nothing after it, and the carried state the reference's
+    partial update (continuing with the block fixed equals the oracle)."""
     bits = 8
-    eb = 5 * slab_eblocks(ch) + 100
-    j = 2 * slab_eblocks(ch) + 4567
+    se = slab_eblocks(ch)
+    eb = 5 * se + 100
+    j = {"mid": 2 * se + 4567, "first": 9, "boundary": 3 * se, "last": eb - 1}[where]
     bx = (bits * 4 + 1) * ch
     xa = synth.stream(eb, bits, ch, "A", seed=43 + ch + bad).reshape(eb * ch, 33)
     xa[j * ch + bad, 0] = 0x5F
