@@ -30,7 +30,13 @@ def main():
     ap.add_argument("--passes", type=int, default=5)
     ap.add_argument("--encode", action="store_true",
                     help="bjxa_encode() of the same stream's PCM instead")
+    ap.add_argument("--alt-env", default=None,
+                    help="NAME=V1,V2: alternate this environment variable between "
+                         "calls (a knob the library reads per call) and report the "
+                         "median per value")
     args = ap.parse_args()
+    if args.alt_env:
+        return alt_rate(args)
     if args.encode:
         return encode_rate(args)
     ch = args.ch
@@ -57,6 +63,33 @@ def main():
                       "MSamples_per_s": round(samples / med / 1e6, 1),
                       "host_GB_per_s": round((len(xa) + dst.nbytes) / med / 1e9, 2),
                       "first_call_ms": round(times[0] * 1e3, 3), "bit_exact": ok}))
+
+
+def alt_rate(args):
+    """Decode calls alternating a per-call library knob, interleaved in one
+    process (box and run drift hit every value alike)."""
+    name, vals = args.alt_env.split("=", 1)
+    vals = vals.split(",")
+    ch = args.ch
+    eb = 2_000_000 if ch == 2 else 4_000_000
+    bits = 8
+    xa = synth.stream(eb, bits, ch, "A", seed=7)
+    hdr = bjxa_amd.xa_header(len(xa), eb * 32, 44100, bits, ch)
+    dst = np.zeros(eb * 64 * ch, dtype=np.uint8)
+    times = {v: [] for v in vals}
+    with bjxa_amd.Decoder() as d:
+        for i in range(args.passes + 1):
+            for v in vals:
+                os.environ[name] = v
+                d.parse_header(hdr)
+                t = time.perf_counter()
+                assert d.decode(dst, xa) == eb
+                if i:
+                    times[v].append(time.perf_counter() - t)
+    print(json.dumps({"api": "bjxa_decode (host buffers)", "channels": ch, "eblocks": eb,
+                      "knob": name, "ms_median": {v: round(float(np.median(t)) * 1e3, 3)
+                                                  for v, t in times.items()},
+                      "ms_all": {v: [round(x * 1e3, 3) for x in t] for v, t in times.items()}}))
 
 
 def encode_rate(args):
