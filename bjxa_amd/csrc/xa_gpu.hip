@@ -1148,8 +1148,11 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 		if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount,
 		    g->device) != hipSuccess || ncu <= 0)
 			ncu = 256;
+		if (ncu > 64 * 32)
+			ncu = 64 * 32;
 		const unsigned oc = DUPLEX_OUT_CUS;
-		std::vector<uint32_t> mo((ncu + 31) / 32, 0u), md((ncu + 31) / 32, 0u);
+		const uint32_t nw = (uint32_t)(ncu + 31) / 32;
+		uint32_t mo[64] = { 0 }, md[64] = { 0 };	/* (no allocation) */
 		const unsigned step = oc > 0 && oc < (unsigned)ncu ? ncu / oc : 1u;
 		for (int c = 0; c < ncu; c++) {
 			const bool out = oc == 0 || (c % step == 0 &&
@@ -1164,9 +1167,9 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 			    hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) ==
 			    hipSuccess;
 		} else if (ok) {
-			if (hipExtStreamCreateWithCUMask(&g->s_out, (uint32_t)mo.size(),
-			    mo.data()) != hipSuccess || hipExtStreamCreateWithCUMask(
-			    &g->s_dec, (uint32_t)md.size(), md.data()) != hipSuccess) {
+			if (hipExtStreamCreateWithCUMask(&g->s_out, nw, mo) !=
+			    hipSuccess || hipExtStreamCreateWithCUMask(&g->s_dec, nw,
+			    md) != hipSuccess) {
 				/* no CU masks here: plain streams (slower, R6-7) */
 				(void)hipGetLastError();
 				if (g->s_out != NULL)
