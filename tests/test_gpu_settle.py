@@ -164,6 +164,54 @@ def test_smaller_stream_reuses_workspace(built):
     assert rec[1] == rec[3] == nxt             # the tag prediction held
 
 
+def test_larger_stream_after_smaller(built):
+    """The other direction of the same hazard: a larger stream after a
+    smaller one in the same workspace puts its records where stale words
+    lie (here, poisoned with the next launch's tag); the changed layout
+    zeroes them first.  Big, small, then big again."""
+    torch = require_gpu()
+    big, small, bits, ch = 2_500_000, 700_000, 8, 2
+    xa_big = synth.stream(big, bits, ch, "W", seed=19)
+    xa_small = synth.stream(small, bits, ch, "A", seed=20)
+    ref_big, st_ref, _, _ = oracle.decode(xa_big, big, bits, ch)
+    ref_small, _, _, _ = oracle.decode(xa_small, small, bits, ch)
+    ws_len = bjxa_amd.decode_workspace_size(big, ch, 0, 0)
+    ws = torch.zeros(ws_len, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(bjxa_amd.STATUS_WORDS, dtype=torch.int32, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    bjxa_amd.workspace_init(ws.data_ptr(), ws_len, sh)
+
+    def decode(xa, eb):
+        src = torch.from_numpy(xa).cuda()
+        dst = torch.full((eb * 64 * ch,), 0x5A, dtype=torch.uint8, device="cuda")
+        bjxa_amd.decode_device(src.data_ptr(), dst.data_ptr(), eb, eb * 32, bits, ch,
+                               ws.data_ptr(), ws_len, status.data_ptr(), (0, 0, 0, 0),
+                               0, 0, sh)
+        torch.cuda.synchronize()
+        return dst.cpu().numpy().view(np.int16), status.cpu().numpy().view(np.uint32).copy()
+
+    got, st = decode(xa_big, big)              # learn the larger layout
+    assert np.array_equal(got, ref_big)
+    n_big = int(st[5])
+    got, st = decode(xa_small, small)
+    assert np.array_equal(got, ref_small)
+    xs = _layout(int(st[5]))[3]
+    rec = ws[xs:xs + 16].cpu().numpy().view(np.uint32)
+    assert rec[1] == rec[3] != 0
+    nxt = (int(rec[1]) + 1) & 0xFFFFFFFF or 1
+    xb = _layout(n_big)[3]
+    nw = (n_big + 63) // 64
+    words = np.empty((nw, 4), dtype=np.uint32)
+    words[:, 0::2] = 0x7FFF8001                # bogus exit state, both channels
+    words[:, 1::2] = nxt
+    ws[xb:xb + 16 * nw].copy_(torch.from_numpy(words.reshape(-1).view(np.uint8)))
+    got, st = decode(xa_big, big)
+    assert np.array_equal(got, ref_big)
+    assert status_state(st) == st_ref
+    rec = ws[xb:xb + 16].cpu().numpy().view(np.uint32)
+    assert rec[1] == rec[3] == nxt             # the tag prediction held
+
+
 @pytest.mark.parametrize("variant", [bjxa_amd.VARIANT_NORECORD, bjxa_amd.VARIANT_NOWAIT])
 def test_batch_boundaries_left_to_tail(built, variant):
     """The batch kernel with the same knobs: every format, cascades."""
