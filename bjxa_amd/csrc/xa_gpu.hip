@@ -259,7 +259,21 @@ bjxa_hip_decode_workspace(uint32_t eblocks, unsigned channels,
 	if (channels != 1 && channels != 2)
 		return 0;
 	plan_chunks(eblocks, channels, tune, &p);
-	return ws_bytes(p.nchunks);
+	uint64_t n = p.nchunks;
+	if (!(tune && tune->chunk)) {
+		/*
+		 * The automatic plan is not monotone in the stream length (C3's
+		 * 5,000,000 eblocks plan 125,000 chunks of 40, 2,600,000 plan
+		 * 130,000 of 20), but no stream of at most `eblocks` plans more
+		 * than min(ceil(eblocks / MIN_CHUNK), lanes) chunks: sized for
+		 * that, the workspace serves every shorter stream too
+		 * (INTEGRATION.md), for at most 24 B per chunk more.
+		 */
+		const uint64_t b = std::min(((uint64_t)eblocks + MIN_CHUNK - 1) /
+		    MIN_CHUNK, (uint64_t)plan_lanes(tune));
+		n = std::max(n, b);
+	}
+	return ws_bytes((uint32_t)n);
 }
 
 __global__ void

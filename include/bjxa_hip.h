@@ -76,7 +76,9 @@ typedef struct {
  */
 #define BJXA_HIP_STATUS_WORDS 8
 
-/* workspace bytes for one stream of `eblocks`; call bjxa_hip_workspace_init
+/* workspace bytes for one stream of `eblocks`, non-decreasing in `eblocks`
+ * under the automatic plan (tune == NULL or tune->chunk == 0), so the same
+ * workspace serves every shorter stream too; call bjxa_hip_workspace_init
  * once before first use; a completed decode leaves it reusable.  A decode
  * whose launch fails re-initialises it itself; after a device fault (an
  * error from the stream) initialise it again before reusing it */

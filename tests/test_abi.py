@@ -159,3 +159,21 @@ def test_batch_argument_checks(built):
     assert r.returncode == 0, r.stderr
     got = [int(v) for v in r.stdout.split()]
     assert got == [errno.EINVAL] * 8 + [errno.ENODEV], got
+
+
+def test_workspace_size_covers_shorter_streams(built):
+    """bjxa_hip_decode_workspace(eb) is non-decreasing in eb (automatic
+    plan), so a workspace sized for a stream also serves every shorter one
+    (INTEGRATION.md), although the plan's chunk count is not monotone (C3's
+    5,000,000 eblocks plan 125,000 chunks, 2,600,000 plan 130,000).  Host
+    arithmetic only, no GPU needed (without one the planner assumes 256
+    CUs)."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    ebs = sorted(set(int(v) for v in rng.integers(1, 60_000_000, 400)) |
+                 {1, 16, 17, 2_097_152, 2_097_153, 2_600_000, 5_000_000})
+    for ch in (1, 2):
+        sizes = [built.decode_workspace_size(eb, ch) for eb in ebs]
+        assert all(a <= b for a, b in zip(sizes, sizes[1:])), ch
+        assert built.decode_workspace_size(2_600_000, ch) <= \
+            built.decode_workspace_size(5_000_000, ch)
