@@ -29,15 +29,21 @@ BATCH = ("C4", "C5", "C5g")
 _HIP = []
 
 
-def raw_buffer(n):
+def raw_buffer(n, flags=None):
     """A uint8 CUDA tensor over a hipMalloc of exactly n bytes (kept for the
-    life of the process)."""
+    life of the process); with `flags`, hipExtMallocWithFlags (4 =
+    hipDeviceMallocContiguous)."""
     if not _HIP:
         h = ctypes.CDLL("libamdhip64.so.7")
         h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        h.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                            ctypes.c_uint]
         _HIP.append(h)
     p = ctypes.c_void_p()
-    assert _HIP[0].hipMalloc(ctypes.byref(p), n) == 0
+    if flags is None:
+        assert _HIP[0].hipMalloc(ctypes.byref(p), n) == 0
+    else:
+        assert _HIP[0].hipExtMallocWithFlags(ctypes.byref(p), n, flags) == 0
 
     class Iface:
         __cuda_array_interface__ = {"shape": (n,), "typestr": "|u1",
@@ -71,11 +77,12 @@ def main():
                          "larger allocations (a multiple of 16)")
     ap.add_argument("--eblocks", type=int, default=0,
                     help="single-stream workloads: override the stream length")
-    ap.add_argument("--layout", default="sep", choices=["sep", "packed", "gaps", "gaps2m",
-                                                        "skew", "pages", "packed_src",
-                                                        "packed_dst", "hipmalloc"],
+    ap.add_argument("--layout", default="sep",
                     help="batches: one allocation per stream buffer (sep) or all "
-                         "streams back to back in one allocation (packed)")
+                         "streams back to back in one allocation (packed); also gaps, "
+                         "gaps2m, skew, pages, packed_src, packed_dst, hipmalloc, and "
+                         "rot<b> / pad<b> (PCM only, one allocation: image i shifted by "
+                         "(37 i mod 64) << b, or images 2^b bytes apart past their size)")
     ap.add_argument("builds", nargs="+")
     args = ap.parse_args()
     batch = args.wl in BATCH or args.wl.startswith(("C3x", "B"))
@@ -95,8 +102,25 @@ def main():
         else:
             inputs = bench.batch_inputs(args.wl, 0, 0, 0, len(bench.batch_specs(args.wl)),
                                         mix=args.mix)
-        if args.layout in ("packed", "gaps", "gaps2m", "skew", "pages", "packed_src",
-                           "packed_dst"):
+        lay = args.layout
+        shift = None
+        if lay.startswith(("rot", "pad")):
+            shift = (lay[:3], int(lay[3:]))
+            lay = "packed_dst"
+        elif lay in ("contig", "contig_sep"):
+            # PCM images back to back in one hipDeviceMallocContiguous
+            # allocation, or each in one of its own
+            shift = (lay, 0)
+            lay = "sep"
+        elif lay.startswith(("grp", "own")):
+            # grp<g>: PCM images back to back in allocations of g images each;
+            # own<m>: each PCM image at the start of an allocation of m MiB
+            shift = (lay[:3], int(lay[3:]))
+            lay = "sep"
+        assert lay in ("sep", "packed", "gaps", "gaps2m", "skew", "pages", "packed_src",
+                       "packed_dst", "hipmalloc"), args.layout
+        if lay in ("packed", "gaps", "gaps2m", "skew", "pages", "packed_src",
+                   "packed_dst"):
             # every stream in one allocation, back to back at 256-B steps
             # (gaps: plus a seeded random gap of 0-255 x 256 B before each;
             # gaps2m: 0-31 x 64 KiB; skew: stream i at +(37 i mod 32) x
@@ -117,24 +141,31 @@ def main():
                     elif args.layout == "skew":
                         o = (o + (1 << 21) - 1) // (1 << 21) * (1 << 21) + \
                             ((37 * k) % 32) * 65536 + (k % 16) * 4096
+                    if shift is not None and shift[0] == "rot":
+                        # image k at k whole strides plus (37 k mod 64) << b
+                        st = (((n + (64 << shift[1]) - 1) >> (shift[1] + 6)) + 1) << \
+                            (shift[1] + 6)
+                        o = k * st + (((37 * k) % 64) << shift[1])
                     offs.append(o)
                     o += (n + 255) // 256 * 256
+                    if shift is not None and shift[0] == "pad":
+                        o += 1 << shift[1]
                 big = torch.empty(o, dtype=torch.uint8, device="cuda")
                 return [big[a:a + n] for a, n in zip(offs, sizes)]
             # (packed_src / packed_dst: only the XA inputs / only the PCM
             # images back to back in one allocation, the other side separate)
-            if args.layout == "packed_dst":
+            if lay == "packed_dst":
                 srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
             else:
                 srcs = carve([x.size for *_, x in inputs])
                 for t_, (*_, x) in zip(srcs, inputs):
                     t_.copy_(torch.from_numpy(x))
-            if args.layout == "packed_src":
+            if lay == "packed_src":
                 dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
                         for _, _, ch, eb, _ in inputs]
             else:
                 dsts = carve([eb * 64 * ch for _, _, ch, eb, _ in inputs])
-        elif args.layout == "hipmalloc":
+        elif lay == "hipmalloc":
             # every buffer a hipMalloc of its own at its exact size (as a C
             # caller would make them), outside torch's caching allocator
             srcs = [raw_buffer(x.size) for *_, x in inputs]
@@ -143,8 +174,27 @@ def main():
             dsts = [raw_buffer(eb * 64 * ch) for _, _, ch, eb, _ in inputs]
         else:
             srcs = [torch.from_numpy(x).cuda() for *_, x in inputs]
-            dsts = [torch.empty(eb * 64 * ch, dtype=torch.uint8, device="cuda")
-                    for _, _, ch, eb, _ in inputs]
+            sizes = [eb * 64 * ch for _, _, ch, eb, _ in inputs]
+            if shift is not None and shift[0] == "grp":
+                dsts = []
+                for i in range(0, len(sizes), shift[1]):
+                    part = sizes[i:i + shift[1]]
+                    big = torch.empty(sum(part), dtype=torch.uint8, device="cuda")
+                    o = 0
+                    for n in part:
+                        dsts.append(big[o:o + n])
+                        o += n
+            elif shift is not None and shift[0] == "contig":
+                big = raw_buffer(sum(sizes), 4)
+                offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+                dsts = [big[int(o):int(o) + n] for o, n in zip(offs, sizes)]
+            elif shift is not None and shift[0] == "contig_sep":
+                dsts = [raw_buffer(n, 4) for n in sizes]
+            elif shift is not None and shift[0] == "own":
+                dsts = [torch.empty(max(n, shift[1] << 20), dtype=torch.uint8,
+                                    device="cuda")[:n] for n in sizes]
+            else:
+                dsts = [torch.empty(n, dtype=torch.uint8, device="cuda") for n in sizes]
         arr = (HipStream * len(inputs))()
         for i, ((_, bits, ch, eb, _), s_, d_) in enumerate(zip(inputs, srcs, dsts)):
             arr[i] = HipStream(s_.data_ptr(), d_.data_ptr(), eb * 32, eb, bits, ch,
