@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <list>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -1265,6 +1266,80 @@ struct in_progress {
 	bool done = false, failed = false, stop = false;
 };
 
+/*
+ * The duplex route's registrations of caller input, process-wide.  A call
+ * registers its input's pages for the call and unregisters them at its end;
+ * another call whose input shares a page with that range must not copy from
+ * it meanwhile (unregistering under its copies would take the pages from
+ * under a transfer that the runtime started as a pinned one).  So a call
+ * whose pages lie inside a live registration shares it (a user count), and
+ * one that overlaps a registration only in part, or one still being made,
+ * waits for it to end.  A call holds at most one entry and waits only
+ * while it holds none, so nothing waits in a cycle.
+ */
+struct host_reg {
+	uintptr_t	a, b;		/* page range */
+	unsigned	users;
+	bool		pending;	/* hipHostRegister still running */
+	bool		ok;		/* registered by us (else: plain copies) */
+};
+
+std::mutex reg_mu;
+std::condition_variable reg_cv;
+std::list<host_reg> regs;
+
+/* the entry covering [a, b) for this call (registered, shared or plain) */
+std::list<host_reg>::iterator
+reg_acquire(uintptr_t a, uintptr_t b)
+{
+	std::unique_lock<std::mutex> l(reg_mu);
+	for (;;) {
+		auto o = regs.end();
+		for (auto it = regs.begin(); it != regs.end(); ++it)
+			if (it->a < b && a < it->b) {
+				o = it;
+				break;
+			}
+		if (o == regs.end())
+			break;
+		if (!o->pending && o->a <= a && b <= o->b) {
+			o->users++;
+			return o;
+		}
+		reg_cv.wait(l);
+	}
+	auto e = regs.insert(regs.end(), host_reg{ a, b, 1u, true, false });
+	l.unlock();
+	const bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterDefault) ==
+	    hipSuccess;
+	if (!ok)
+		(void)hipGetLastError();	/* (already pinned, say): plain copies */
+	l.lock();
+	e->pending = false;
+	e->ok = ok;
+	reg_cv.notify_all();
+	return e;
+}
+
+void
+reg_release(std::list<host_reg>::iterator e)
+{
+	std::lock_guard<std::mutex> l(reg_mu);
+	if (--e->users != 0)
+		return;
+	if (e->ok)
+		(void)hipHostUnregister((void *)e->a);
+	regs.erase(e);
+	reg_cv.notify_all();
+}
+
+/* one call's hold on its entry */
+struct reg_hold {
+	std::list<host_reg>::iterator e;
+	reg_hold(uintptr_t a, uintptr_t b) : e(reg_acquire(a, b)) {}
+	~reg_hold() { reg_release(e); }
+};
+
 }	/* namespace */
 
 /* BJXA_DUPLEX_TRACE=1: per-slab host timestamps on stderr (diagnostic) */
@@ -1290,7 +1365,8 @@ duplex_trace(void)
  * a true asynchronous copy at the link rate (from pageable memory the
  * runtime's staged copies of 8 MiB ran at ~22 GB/s and paced the whole
  * call); where registration fails (memory already pinned or registered,
- * say) the copies stay pageable.
+ * say) the copies stay pageable.  Calls whose inputs share pages share or
+ * wait for each other's registration (reg_acquire).
  *   in_range(k, &off, &len)    slab k's input bytes [off, off + len)
  *   gpu(k, slot)               enqueue slab k's kernel on g->s_dec (after
  *                              ev_in[k]) and its copy-out into the device
@@ -1335,16 +1411,9 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	std::vector<double> t_in(n, 0.0), t_iss(n, 0.0), t_out(n, 0.0), t_cp(n, 0.0);
 	const double t0 = tr ? trace_ms() : 0.0;
 
-	void *reg_base = NULL;
-	{
-		const uintptr_t a = (uintptr_t)src & ~(uintptr_t)4095;
-		const uintptr_t b = ((uintptr_t)src + in_bytes + 4095) & ~(uintptr_t)4095;
-		if (hipHostRegister((void *)a, b - a, hipHostRegisterDefault) ==
-		    hipSuccess)
-			reg_base = (void *)a;
-		else
-			(void)hipGetLastError();
-	}
+	/* (released on return, after the streams are synchronised) */
+	reg_hold reg((uintptr_t)src & ~(uintptr_t)4095,
+	    ((uintptr_t)src + in_bytes + 4095) & ~(uintptr_t)4095);
 	in_progress ip;
 	const int dev = g->device;
 	uint8_t *d_in = (uint8_t *)g->d_in;
@@ -1380,8 +1449,6 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	try {
 		input = std::thread(input_body);
 	} catch (...) {
-		if (reg_base != NULL)
-			(void)hipHostUnregister(reg_base);
 		errno = EAGAIN;
 		return -1;
 	}
@@ -1435,8 +1502,6 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	const bool synced = hipStreamSynchronize(g->s_in) == hipSuccess &&
 	    hipStreamSynchronize(g->s_dec) == hipSuccess &&
 	    hipStreamSynchronize(g->s_out) == hipSuccess;
-	if (reg_base != NULL)
-		(void)hipHostUnregister(reg_base);
 	if (tr) {
 		fprintf(stderr, "duplex %zu slabs, done %.3f ms\n", n, trace_ms() - t0);
 		for (size_t k = 0; k < n; k++)

@@ -211,3 +211,43 @@ def test_duplex_concurrent_codecs(built):
     assert not errs, errs
     for (xa, eb, bits, ch, ref), got in zip(jobs, out):
         assert np.array_equal(got.view(np.int16), ref)
+
+
+def _threads(fns):
+    import threading
+    out, errs = [None] * len(fns), []
+
+    def run(i):
+        try:
+            out[i] = fns[i]()
+        except Exception as e:      # reported below
+            errs.append(e)
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(fns))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    return out
+
+
+def test_duplex_shared_input_pages(built):
+    """Calls whose inputs share host pages (xa_gpu.hip reg_acquire): three
+    threads decoding the same buffer at once share one registration, and
+    two threads decoding the two halves of one buffer, split off a page
+    boundary so one page holds both, take turns with theirs.  A call that
+    unregistered pages under another's transfers would corrupt or fault
+    it; every result bit-exact."""
+    eb = 4 * slab_eblocks(2) + 77
+    xa = synth.stream(2 * eb, 8, 2, "A", seed=48)
+    cut = eb * 66                                   # 66 B per stereo eblock
+    assert cut % 4096 != 0
+    halves = [xa[:cut], xa[cut:]]
+    refs = [oracle.decode(h, eb, 8, 2)[0] for h in halves]
+    got = _threads([lambda: host_decode(halves[0], eb, 8, 2, eb * 32)] * 3)
+    for g in got:
+        assert np.array_equal(g.view(np.int16), refs[0])
+    got = _threads([lambda k=k: host_decode(halves[k], eb, 8, 2, eb * 32)
+                    for k in (0, 1, 0, 1)])
+    for k, g in zip((0, 1, 0, 1), got):
+        assert np.array_equal(g.view(np.int16), refs[k])
