@@ -10,6 +10,7 @@
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <stdio.h>
 
@@ -835,7 +836,7 @@ struct bjxa__gpu {
 	bool		ws_stale;	/* a call failed: initialise the
 					 * workspace again before the next */
 	/* the duplex route of large calls (duplex_decode), made on first use */
-	hipStream_t	s_in, s_out, s_dec;
+	hipStream_t	s_out, s_dec;
 	uint8_t		*h_stage;	/* pinned: DUPLEX_SLOTS staging slots */
 	uint8_t		*d_stage;	/* its device view */
 	uint32_t	*d_sst;		/* per-slab status words */
@@ -918,11 +919,9 @@ bjxa__gpu_free(struct bjxa__gpu *g)
 	(void)hipFree(g->d_status);
 	if (g->h_small != NULL)
 		(void)hipHostFree(g->h_small);
-	if (g->s_in != NULL) {
-		(void)hipStreamSynchronize(g->s_in);
+	if (g->s_out != NULL) {
 		(void)hipStreamSynchronize(g->s_out);
 		(void)hipStreamSynchronize(g->s_dec);
-		(void)hipStreamDestroy(g->s_in);
 		(void)hipStreamDestroy(g->s_out);
 		(void)hipStreamDestroy(g->s_dec);
 	}
@@ -1067,17 +1066,19 @@ call_buffers(struct bjxa__gpu *g, uint32_t eblocks, uint32_t ws_eblocks,
  * profiles/r06_zc_duplex.json).  So such a call runs in slabs of
  * DUPLEX_SLAB PCM bytes:
  *
- *   input thread   H2D of slab k's XA from the caller's buffer, registered
- *                  for the call (copy engine)
- *   g->s_dec       decode slab k (K1 + tail); its entry state is read on
- *                  the device from slab k-1's status words
- *   g->s_out       a copy kernel stores slab k's PCM and status into a
- *                  pinned staging slot, on CUs of its own (its stores wait
- *                  on PCIe and would hold up a decode sharing their CUs)
- *   calling thread and the copy pool: slot -> the caller's dst
+ *   g->s_dec       H2D of slab k's XA from the caller's buffer, registered
+ *                  for the call (copy engine), then decode slab k (K1 +
+ *                  tail); its entry state is read on the device from slab
+ *                  k-1's status words
+ *   g->s_out       a copy kernel stores slab k's PCM straight into the
+ *                  caller's dst when that could be registered (direct), or
+ *                  into a pinned staging slot, and its status into the
+ *                  slot's header, on CUs of its own (its stores wait on PCIe
+ *                  and would hold up a decode sharing their CUs)
+ *   calling thread and the copy pool: slot -> the caller's dst (staging)
  *
- * A slot is reused once its host copy is done.  A slab whose status
- * reports a failing block ends the copies at that eblock, as the serial
+ * A slot is reused once the host is done with it.  A slab whose status
+ * reports a failing block ends the output at that eblock, as the serial
  * route does; nothing is written to dst past it.  BJXA_DUPLEX=0 (read at
  * the first call) keeps every call on the serial route.
  */
@@ -1118,6 +1119,53 @@ xa_slab_out(const uint4 *src, uint4 *dst, uint64_t n16, const uint32_t *st,
 			dst[i + 256u * u] = src[i + 256u * u];
 }
 
+/*
+ * The direct form of xa_slab_out, for a decode whose output (the caller's
+ * buffer) is registered: the slab's PCM goes straight into it, which spares
+ * the host copy out of staging (that copy slowed the kernel's PCIe writes
+ * by ~15 %, tools/copyout_probe2.hip).  It writes the slab's `nbytes` cut
+ * at its first failing block (its status), and nothing if an earlier slab
+ * failed: stop_prev is the word the previous slab's copy-out left (NULL for
+ * the first slab), stop_cur this slab's, so no PCM past the failing block
+ * reaches the caller, as on the serial route.  The status words go to the
+ * slot header for the host, as in xa_slab_out.
+ */
+__global__ __launch_bounds__(256) void
+xa_slab_direct(const uint4 *src, uint8_t *dst, uint64_t nbytes,
+    const uint32_t *st, uint32_t *st_out, const uint32_t *stop_prev,
+    uint32_t *stop_cur, uint32_t ob, uint32_t ch)
+{
+	const uint32_t err = st[XA_ST_ERR];
+	const bool stopped = stop_prev != nullptr && *stop_prev != 0u;
+	if (blockIdx.x == 0 && threadIdx.x < XA_ST_WORDS)
+		st_out[threadIdx.x] = st[threadIdx.x];
+	if (blockIdx.x == 0 && threadIdx.x == 0)
+		*stop_cur = stopped || err != 0xffffffffu ? 1u : 0u;
+	if (stopped)
+		return;
+	if (err != 0xffffffffu)
+		nbytes = min(nbytes, (uint64_t)(err / ch) * ob);
+	const uint64_t n16 = nbytes / 16u;
+	uint4 *d = (uint4 *)dst;
+	const uint64_t step = (uint64_t)gridDim.x * 256u * SLAB_OUT_U;
+	uint64_t i = blockIdx.x * 256ull * SLAB_OUT_U + threadIdx.x;
+	for (; i + 256u * (SLAB_OUT_U - 1) < n16; i += step) {
+		uint4 v[SLAB_OUT_U];
+#pragma unroll
+		for (int u = 0; u < SLAB_OUT_U; u++)
+			v[u] = src[i + 256u * u];
+#pragma unroll
+		for (int u = 0; u < SLAB_OUT_U; u++)
+			d[i + 256u * u] = v[u];
+	}
+	for (int u = 0; u < SLAB_OUT_U; u++)	/* the last, partial tile */
+		if (i + 256u * u < n16)
+			d[i + 256u * u] = src[i + 256u * u];
+	if (blockIdx.x == 0 && threadIdx.x == 0)	/* a cut last block */
+		for (uint64_t b = n16 * 16u; b < nbytes; b++)
+			dst[b] = ((const uint8_t *)src)[b];
+}
+
 static bool
 duplex_enabled(void)
 {
@@ -1128,6 +1176,37 @@ duplex_enabled(void)
 		on = e == NULL || strcmp(e, "0") != 0;
 	});
 	return on;
+}
+
+/*
+ * Are the pages of [p, p + len) in memory (32 pages sampled)?  Registering
+ * a buffer whose pages were never touched faults every one of them in, one
+ * thread, inside the call: a fresh 256 MB output took the direct route to
+ * 16.8 ms against 9.7 through staging, whose host copies fault them in on
+ * many threads (tools/host_rate.py --fresh, R6-7).  Such a buffer goes
+ * through staging.
+ */
+static bool
+resident(const void *p, size_t len)
+{
+	const uintptr_t pg = 4096, a = (uintptr_t)p & ~(pg - 1);
+	const uintptr_t npg = ((uintptr_t)p + len - a + pg - 1) / pg;
+	for (uintptr_t i = 0; i < 32; i++) {
+		unsigned char v = 0;
+		const uintptr_t q = a + (npg * i / 32) * pg;
+		if (mincore((void *)q, pg, &v) != 0 || (v & 1u) == 0)
+			return false;
+	}
+	return true;
+}
+
+/* BJXA_DUPLEX_DIRECT=0: decodes always copy out through staging (read per
+ * call, so one process can A/B it) */
+static bool
+duplex_direct(void)
+{
+	const char *e = getenv("BJXA_DUPLEX_DIRECT");
+	return e == NULL || strcmp(e, "0") != 0;
 }
 
 static std::mutex duplex_pool_mu;
@@ -1151,7 +1230,7 @@ duplex_copy(uint8_t *to, const uint8_t *from, size_t len)
 static int
 duplex_setup(struct bjxa__gpu *g, size_t nslab)
 {
-	if (g->s_in == NULL) {
+	if (g->s_out == NULL) {
 		/*
 		 * The copy-out kernel's stores go over PCIe and back up every
 		 * CU's memory pipeline they run on, so a decode kernel sharing
@@ -1174,14 +1253,13 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 			    (unsigned)(c / step) < oc);
 			(out ? mo : md)[c / 32] |= 1u << (c % 32);
 		}
-		bool ok = hipStreamCreateWithFlags(&g->s_in, hipStreamNonBlocking) ==
-		    hipSuccess;
+		bool ok = true;
 		if (oc == 0 || oc >= (unsigned)ncu) {
-			ok = ok && hipStreamCreateWithFlags(&g->s_out,
+			ok = hipStreamCreateWithFlags(&g->s_out,
 			    hipStreamNonBlocking) == hipSuccess &&
 			    hipStreamCreateWithFlags(&g->s_dec, hipStreamNonBlocking) ==
 			    hipSuccess;
-		} else if (ok) {
+		} else {
 			if (hipExtStreamCreateWithCUMask(&g->s_out, nw, mo) !=
 			    hipSuccess || hipExtStreamCreateWithCUMask(&g->s_dec, nw,
 			    md) != hipSuccess) {
@@ -1198,13 +1276,11 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 		}
 		if (!ok) {
 			(void)hipGetLastError();
-			if (g->s_in != NULL)
-				(void)hipStreamDestroy(g->s_in);
 			if (g->s_out != NULL)
 				(void)hipStreamDestroy(g->s_out);
 			if (g->s_dec != NULL)
 				(void)hipStreamDestroy(g->s_dec);
-			g->s_in = g->s_out = g->s_dec = NULL;
+			g->s_out = g->s_dec = NULL;
 			return io_fail();
 		}
 	}
@@ -1223,10 +1299,11 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 		}
 	}
 	if (g->sst_cap < nslab) {
+		/* per slab its status words, then per slab a stop word */
 		(void)hipFree(g->d_sst);
 		g->d_sst = NULL;
 		g->sst_cap = 0;
-		if (hipMalloc((void **)&g->d_sst, nslab * XA_ST_WORDS * 4) !=
+		if (hipMalloc((void **)&g->d_sst, nslab * (XA_ST_WORDS + 1) * 4) !=
 		    hipSuccess) {
 			g->d_sst = NULL;
 			errno = ENOMEM;
@@ -1257,25 +1334,18 @@ struct event_set {
 	}
 };
 
-/* the input thread's progress: slabs whose H2D is enqueued and its event
- * recorded */
-struct in_progress {
-	std::mutex m;
-	std::condition_variable cv;
-	size_t ready = 0;
-	bool done = false, failed = false, stop = false;
-};
-
 /*
- * The duplex route's registrations of caller input, process-wide.  A call
- * registers its input's pages for the call and unregisters them at its end;
- * another call whose input shares a page with that range must not copy from
- * it meanwhile (unregistering under its copies would take the pages from
- * under a transfer that the runtime started as a pinned one).  So a call
- * whose pages lie inside a live registration shares it (a user count), and
- * one that overlaps a registration only in part, or one still being made,
- * waits for it to end.  A call holds at most one entry and waits only
- * while it holds none, so nothing waits in a cycle.
+ * The duplex route's registrations of caller memory, process-wide.  A call
+ * registers its input's pages (and, for a decode written straight into the
+ * caller's buffer, its output's) for the call and unregisters them at its
+ * end; another call whose buffers share a page with such a range must not
+ * transfer to or from it meanwhile (unregistering under its transfers would
+ * take the pages from under a transfer that the runtime or a kernel started
+ * on pinned memory).  So a range that lies inside a live registration shares
+ * it (a user count), and one that overlaps a registration only in part, or
+ * one still being made, waits for it to end.  A call takes all its entries
+ * at once and waits only while it holds none, so nothing waits in a cycle.
+ * Entries never overlap one another.
  */
 struct host_reg {
 	uintptr_t	a, b;		/* page range */
@@ -1288,56 +1358,99 @@ std::mutex reg_mu;
 std::condition_variable reg_cv;
 std::list<host_reg> regs;
 
-/* the entry covering [a, b) for this call (registered, shared or plain) */
-std::list<host_reg>::iterator
-reg_acquire(uintptr_t a, uintptr_t b)
-{
-	std::unique_lock<std::mutex> l(reg_mu);
-	for (;;) {
-		auto o = regs.end();
-		for (auto it = regs.begin(); it != regs.end(); ++it)
-			if (it->a < b && a < it->b) {
-				o = it;
-				break;
-			}
-		if (o == regs.end())
-			break;
-		if (!o->pending && o->a <= a && b <= o->b) {
-			o->users++;
-			return o;
-		}
-		reg_cv.wait(l);
-	}
-	auto e = regs.insert(regs.end(), host_reg{ a, b, 1u, true, false });
-	l.unlock();
-	const bool ok = hipHostRegister((void *)a, b - a, hipHostRegisterDefault) ==
-	    hipSuccess;
-	if (!ok)
-		(void)hipGetLastError();	/* (already pinned, say): plain copies */
-	l.lock();
-	e->pending = false;
-	e->ok = ok;
-	reg_cv.notify_all();
-	return e;
-}
-
-void
-reg_release(std::list<host_reg>::iterator e)
-{
-	std::lock_guard<std::mutex> l(reg_mu);
-	if (--e->users != 0)
-		return;
-	if (e->ok)
-		(void)hipHostUnregister((void *)e->a);
-	regs.erase(e);
-	reg_cv.notify_all();
-}
-
-/* one call's hold on its entry */
+/* one call's hold on the entries covering its ranges (registered, shared
+ * or plain); ranges are page-rounded here and merged when they touch */
 struct reg_hold {
-	std::list<host_reg>::iterator e;
-	reg_hold(uintptr_t a, uintptr_t b) : e(reg_acquire(a, b)) {}
-	~reg_hold() { reg_release(e); }
+	std::list<host_reg>::iterator e[2];
+	unsigned n = 0;
+
+	reg_hold(const void *p0, size_t n0, const void *p1, size_t n1)
+	{
+		uintptr_t r[2][2];
+		unsigned nr = 0;
+		const void *p[2] = { p0, p1 };
+		const size_t len[2] = { n0, n1 };
+		for (int i = 0; i < 2; i++)
+			if (p[i] != NULL && len[i] != 0) {
+				r[nr][0] = (uintptr_t)p[i] & ~(uintptr_t)4095;
+				r[nr][1] = ((uintptr_t)p[i] + len[i] + 4095) &
+				    ~(uintptr_t)4095;
+				nr++;
+			}
+		if (nr == 2 && r[0][0] <= r[1][1] && r[1][0] <= r[0][1]) {
+			r[0][0] = std::min(r[0][0], r[1][0]);
+			r[0][1] = std::max(r[0][1], r[1][1]);
+			nr = 1;
+		}
+		bool mine[2] = { false, false };
+		std::unique_lock<std::mutex> l(reg_mu);
+		for (;;) {
+			bool wait = false;
+			for (unsigned i = 0; i < nr && !wait; i++)
+				for (const host_reg &h : regs)
+					if (h.a < r[i][1] && r[i][0] < h.b &&
+					    (h.pending || r[i][0] < h.a || h.b < r[i][1])) {
+						wait = true;
+						break;
+					}
+			if (!wait)
+				break;
+			reg_cv.wait(l);
+		}
+		for (unsigned i = 0; i < nr; i++) {
+			auto it = regs.begin();
+			while (it != regs.end() && !(it->a <= r[i][0] && r[i][1] <= it->b))
+				++it;
+			if (it != regs.end()) {
+				it->users++;
+			} else {
+				it = regs.insert(regs.end(), host_reg{ r[i][0], r[i][1], 1u,
+				    true, false });
+				mine[i] = true;
+			}
+			e[n++] = it;
+		}
+		l.unlock();
+		bool ok[2] = { false, false };
+		for (unsigned i = 0; i < n; i++)
+			if (mine[i]) {
+				ok[i] = hipHostRegister((void *)e[i]->a, e[i]->b - e[i]->a,
+				    hipHostRegisterDefault) == hipSuccess;
+				if (!ok[i])	/* (already pinned, say): plain copies */
+					(void)hipGetLastError();
+			}
+		l.lock();
+		for (unsigned i = 0; i < n; i++)
+			if (mine[i]) {
+				e[i]->pending = false;
+				e[i]->ok = ok[i];
+			}
+		reg_cv.notify_all();
+	}
+
+	~reg_hold()
+	{
+		std::lock_guard<std::mutex> l(reg_mu);
+		for (unsigned i = 0; i < n; i++) {
+			if (--e[i]->users != 0)
+				continue;
+			if (e[i]->ok)
+				(void)hipHostUnregister((void *)e[i]->a);
+			regs.erase(e[i]);
+		}
+		reg_cv.notify_all();
+	}
+
+	/* is [p, p + len) inside an entry this call holds that we registered? */
+	bool registered(const void *p, size_t len) const
+	{
+		std::lock_guard<std::mutex> l(reg_mu);
+		for (unsigned i = 0; i < n; i++)
+			if (e[i]->ok && e[i]->a <= (uintptr_t)p &&
+			    (uintptr_t)p + len <= e[i]->b)
+				return true;
+		return false;
+	}
 };
 
 }	/* namespace */
@@ -1360,38 +1473,53 @@ duplex_trace(void)
 }
 
 /*
- * One duplex call over n slabs (decode or encode).  The caller's input
- * (in_bytes at src) is registered for the call, so that each slab's H2D is
- * a true asynchronous copy at the link rate (from pageable memory the
- * runtime's staged copies of 8 MiB ran at ~22 GB/s and paced the whole
- * call); where registration fails (memory already pinned or registered,
- * say) the copies stay pageable.  Calls whose inputs share pages share or
- * wait for each other's registration (reg_acquire).
+ * One duplex call over n slabs (decode or encode).  Per slab, on the
+ * decode stream: its input H2D, then its kernel; on the copy-out stream,
+ * once that kernel is done, its copy-out; the host keeps DUPLEX_SLOTS slabs
+ * in flight and reaps them in order.  The input shares the decode stream
+ * because an H2D on a stream of its own, behind an event the decode waits
+ * on, started only as a copy-out kernel ended (kernel + copy traces: the
+ * whole route then ran one stage at a time; -3 to -4 % on the call with
+ * the input on the decode stream, R6-7).  The caller's input (in_bytes at
+ * src) is registered for the call, so that each H2D is a true asynchronous
+ * copy at the link rate (from pageable memory the runtime's staged copies
+ * of 8 MiB ran at ~22 GB/s); where registration fails (memory already
+ * pinned or registered, say) the copies stay pageable.  With `out`
+ * (out_bytes), the caller's output is registered too, and where that works
+ * *d_direct is its device view, which the copy-out then writes instead of
+ * staging (else NULL).  Calls whose buffers share pages share or wait for
+ * each other's registrations (reg_hold).
  *   in_range(k, &off, &len)    slab k's input bytes [off, off + len)
- *   gpu(k, slot)               enqueue slab k's kernel on g->s_dec (after
- *                              ev_in[k]) and its copy-out into the device
- *                              view of staging slot `slot` on g->s_out;
- *                              false on failure
- *   host(k, slot)              the calling thread's part once slab k is in
- *                              its slot: copy it out; returns 1 to go on,
- *                              0 to stop early (an error the caller
- *                              reports), -1 on failure
+ *   gpu(k, slot, ev, sd)       enqueue slab k's kernel on sd (the decode
+ *                              stream, after its input), record ev there,
+ *                              and its copy-out (into the device view of
+ *                              staging slot `slot`, or *d_direct) on
+ *                              g->s_out after ev; false on failure
+ *   host(k, slot)              the calling thread's part once slab k's
+ *                              copy-out is done: copy it out of its slot
+ *                              (staging) or check its status; returns 1
+ *                              to go on, 0 to stop early (an error the
+ *                              caller reports), -1 on failure
  * Returns 0 or -1/errno; every enqueued operation has finished on return.
  */
 template <class InRange, class Gpu, class Host>
 static int
 duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
-    InRange &&in_range, Gpu &&gpu, Host &&host);
+    uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
+    Gpu &&gpu, Host &&host);
 
-/* (the C ABI lets no exception out: allocations and the input thread may
- * fail before anything is enqueued, and nothing after that throws) */
+/* (the C ABI lets no exception out: allocations may fail before anything
+ * is enqueued, and nothing after that throws) */
 template <class InRange, class Gpu, class Host>
 static int
 duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
-    InRange &&in_range, Gpu &&gpu, Host &&host)
+    uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
+    Gpu &&gpu, Host &&host)
 {
+	*d_direct = NULL;
 	try {
-		return duplex_run_(g, n, src, in_bytes, in_range, gpu, host);
+		return duplex_run_(g, n, src, in_bytes, out, out_bytes, d_direct,
+		    in_range, gpu, host);
 	} catch (...) {
 		errno = ENOMEM;
 		return -1;
@@ -1401,69 +1529,37 @@ duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 template <class InRange, class Gpu, class Host>
 static int
 duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
-    InRange &&in_range, Gpu &&gpu, Host &&host)
+    uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
+    Gpu &&gpu, Host &&host)
 {
-	event_set evs(3 * n);	/* in, kernel done, out */
+	event_set evs(2 * n);	/* kernel done, copy-out done */
 	if (!evs.ok)
 		return io_fail();
-	hipEvent_t *ev_in = evs.ev.data(), *ev_dec = ev_in + n, *ev_out = ev_dec + n;
+	hipEvent_t *ev_dec = evs.ev.data(), *ev_out = ev_dec + n;
 	const bool tr = duplex_trace();
 	std::vector<double> t_in(n, 0.0), t_iss(n, 0.0), t_out(n, 0.0), t_cp(n, 0.0);
 	const double t0 = tr ? trace_ms() : 0.0;
 
 	/* (released on return, after the streams are synchronised) */
-	reg_hold reg((uintptr_t)src & ~(uintptr_t)4095,
-	    ((uintptr_t)src + in_bytes + 4095) & ~(uintptr_t)4095);
-	in_progress ip;
-	const int dev = g->device;
-	uint8_t *d_in = (uint8_t *)g->d_in;
-	hipStream_t s_in = g->s_in;
-	auto input_body = [&, dev, d_in, s_in] {
-		device_scope on(dev);
-		for (size_t k = 0; k < n; k++) {
-			{
-				std::lock_guard<std::mutex> l(ip.m);
-				if (ip.stop)
-					break;
-			}
-			size_t off, len;
-			in_range(k, &off, &len);
-			const bool ok = hipMemcpyAsync(d_in + off, src + off, len,
-			    hipMemcpyHostToDevice, s_in) == hipSuccess &&
-			    hipEventRecord(ev_in[k], s_in) == hipSuccess;
-			if (tr)
-				t_in[k] = trace_ms() - t0;
-			std::lock_guard<std::mutex> l(ip.m);
-			if (!ok) {
-				ip.failed = true;
-				break;
-			}
-			ip.ready = k + 1;
-			ip.cv.notify_all();
+	reg_hold reg(src, in_bytes, out, out_bytes);
+	if (out != NULL && reg.registered(out, out_bytes)) {
+		if (hipHostGetDevicePointer((void **)d_direct, out, 0) != hipSuccess) {
+			(void)hipGetLastError();
+			*d_direct = NULL;
 		}
-		std::lock_guard<std::mutex> l(ip.m);
-		ip.done = true;
-		ip.cv.notify_all();
-	};
-	std::thread input;
-	try {
-		input = std::thread(input_body);
-	} catch (...) {
-		errno = EAGAIN;
-		return -1;
 	}
-
+	uint8_t *d_in = (uint8_t *)g->d_in;
 	auto issue = [&](size_t k) -> bool {
-		{
-			std::unique_lock<std::mutex> l(ip.m);
-			ip.cv.wait(l, [&] { return ip.ready > k || ip.done; });
-			if (ip.ready <= k)
-				return false;
-		}
+		size_t off, len;
+		in_range(k, &off, &len);
+		if (hipMemcpyAsync(d_in + off, src + off, len, hipMemcpyHostToDevice,
+		    g->s_dec) != hipSuccess)
+			return false;
+		if (tr)
+			t_in[k] = trace_ms() - t0;
 		uint8_t *slot = g->d_stage + (k % DUPLEX_SLOTS) *
 		    (DUPLEX_HDR + DUPLEX_SLAB);
-		if (hipStreamWaitEvent(g->s_dec, ev_in[k], 0) != hipSuccess ||
-		    !gpu(k, slot, ev_dec[k]) ||
+		if (!gpu(k, slot, ev_dec[k], g->s_dec) ||
 		    hipEventRecord(ev_out[k], g->s_out) != hipSuccess)
 			return false;
 		if (tr)
@@ -1492,15 +1588,8 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 		if (k + DUPLEX_SLOTS < n)
 			ok = issue(k + DUPLEX_SLOTS);
 	}
-	{
-		std::lock_guard<std::mutex> l(ip.m);
-		ip.stop = true;
-	}
-	input.join();
-	ok = ok && !ip.failed;
 	/* everything enqueued has to finish before the buffers are reused */
-	const bool synced = hipStreamSynchronize(g->s_in) == hipSuccess &&
-	    hipStreamSynchronize(g->s_dec) == hipSuccess &&
+	const bool synced = hipStreamSynchronize(g->s_dec) == hipSuccess &&
 	    hipStreamSynchronize(g->s_out) == hipSuccess;
 	if (tr) {
 		fprintf(stderr, "duplex %zu slabs, done %.3f ms\n", n, trace_ms() - t0);
@@ -1529,11 +1618,19 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 	auto slab_eb = [&](size_t k) {
 		return (uint32_t)std::min((size_t)eblocks - k * se, (size_t)se);
 	};
+	/* the PCM straight into the caller's buffer where it can be registered,
+	 * is 16-B aligned (the copy-out's stores) and is already in memory;
+	 * else through staging */
+	const bool direct = duplex_direct() && ((uintptr_t)dst & 15u) == 0 &&
+	    resident(dst, (size_t)dst_bytes);
+	uint32_t *stop = g->d_sst + g->sst_cap * XA_ST_WORDS;
+	uint8_t *d_dir = NULL;
 	const int r = duplex_run(g, n, src, (size_t)eblocks * ebsz,
+	    direct ? dst : NULL, (size_t)dst_bytes, &d_dir,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ebsz;
 		*len = slab_eb(k) * ebsz;
-	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done) -> bool {
+	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done, hipStream_t sd) -> bool {
 		const uint32_t e0 = (uint32_t)(k * se), ek = slab_eb(k);
 		bjxa_hip_stream_t s;
 		memset(&s, 0, sizeof s);
@@ -1545,18 +1642,37 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 		s.channels = (uint8_t)ch;
 		memcpy(s.state, state, sizeof s.state);
 		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
-		if (decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, g->s_dec,
+		if (decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, sd,
 		    k > 0 ? sst - XA_ST_WORDS : NULL) < 0 ||
-		    hipEventRecord(ev_done, g->s_dec) != hipSuccess ||
+		    hipEventRecord(ev_done, sd) != hipSuccess ||
 		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
 			return false;
-		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256),
-		    0, g->s_out, (const uint4 *)s.d_dst, (uint4 *)(slot + DUPLEX_HDR),
-		    (uint64_t)ek * ob / 16u, sst, (uint32_t *)slot);
+		if (d_dir != NULL) {
+			const size_t lo = (size_t)e0 * ob;
+			const size_t hi = std::min((size_t)dst_bytes, lo + (size_t)ek * ob);
+			hipLaunchKernelGGL(xa_slab_direct, dim3(2 * DUPLEX_OUT_CUS),
+			    dim3(256), 0, g->s_out, (const uint4 *)s.d_dst, d_dir + lo,
+			    (uint64_t)(hi > lo ? hi - lo : 0), sst, (uint32_t *)slot,
+			    k > 0 ? stop + k - 1 : (const uint32_t *)NULL, stop + k,
+			    (uint32_t)ob, (uint32_t)ch);
+		} else {
+			hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS),
+			    dim3(256), 0, g->s_out, (const uint4 *)s.d_dst,
+			    (uint4 *)(slot + DUPLEX_HDR), (uint64_t)ek * ob / 16u, sst,
+			    (uint32_t *)slot);
+		}
 		return hipGetLastError() == hipSuccess;
 	}, [&](size_t k, const uint8_t *slot) -> int {
 		uint32_t st[XA_ST_WORDS];
 		memcpy(st, (const void *)slot, sizeof st);
+		if (d_dir != NULL) {	/* the kernel wrote the PCM, and cut it */
+			if (st[XA_ST_ERR] != 0xffffffffu) {
+				err = (uint32_t)(k * se * ch) + st[XA_ST_ERR];
+				return 0;
+			}
+			memcpy(fin, st, sizeof fin);
+			return 1;
+		}
 		const size_t lo = k * se * ob;
 		size_t hi = std::min((size_t)dst_bytes, (k * se + slab_eb(k)) * ob);
 		if (st[XA_ST_ERR] != 0xffffffffu) {
@@ -1603,17 +1719,18 @@ duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
 		return std::min((uint64_t)frames - (uint64_t)k * se * 32u,
 		    (uint64_t)se * 32u);
 	};
-	return duplex_run(g, n, src, in_bytes,
+	uint8_t *d_dir = NULL;	/* (XA through staging: not the long direction) */
+	return duplex_run(g, n, src, in_bytes, NULL, 0, &d_dir,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ib;
 		*len = (size_t)slab_frames(k) * 2u * ch;
-	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done) -> bool {
+	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done, hipStream_t sd) -> bool {
 		const uint64_t fk = slab_frames(k);
 		const size_t xk = (size_t)((fk + 31) / 32) * ebsz;
 		uint8_t *d_xa = (uint8_t *)g->d_out + k * se * ebsz;
 		if (bjxa_hip_encode_async((uint8_t *)g->d_in + k * se * ib, fk, bits,
-		    ch, d_xa, g->s_dec) < 0 ||
-		    hipEventRecord(ev_done, g->s_dec) != hipSuccess ||
+		    ch, d_xa, sd) < 0 ||
+		    hipEventRecord(ev_done, sd) != hipSuccess ||
 		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
 			return false;
 		/* whole 16-B pieces (the slot has room past the slab's XA) */

@@ -39,9 +39,21 @@ def host_decode(xa, eb, bits, ch, frames, state=(0, 0, 0, 0), fill=0x5A):
     return dst
 
 
+ROUTES = ["direct", "staging"]
+
+
+def route_env(monkeypatch, route):
+    """The PCM straight into the registered caller buffer (direct, the
+    default for a resident 16-B aligned dst) or through pinned staging and
+    host copies (BJXA_DUPLEX_DIRECT=0, read per call)."""
+    monkeypatch.setenv("BJXA_DUPLEX_DIRECT", "1" if route == "direct" else "0")
+
+
+@pytest.mark.parametrize("route", ROUTES)
 @pytest.mark.parametrize("bits,ch", [(8, 2), (4, 2), (6, 1), (8, 1)])
-def test_duplex_matches_oracle(built, bits, ch):
+def test_duplex_matches_oracle(built, bits, ch, route, monkeypatch):
     """Five slabs and a ragged sixth, the last block cut, a header state."""
+    route_env(monkeypatch, route)
     eb = 5 * slab_eblocks(ch) + 12_345
     frames = eb * 32 - 7
     state = (1234, -4321, -32768, 32767)
@@ -81,15 +93,20 @@ def test_duplex_chained_call(built):
     assert np.array_equal(out.view(np.int16), ref)
 
 
+@pytest.mark.parametrize("route", ROUTES)
 @pytest.mark.parametrize("ch,bad,where", [(2, 0, "mid"), (2, 1, "mid"), (1, 0, "mid"),
                                           (2, 1, "first"), (2, 0, "boundary"),
                                           (1, 0, "boundary"), (2, 1, "last")])
-def test_duplex_invalid_profile_mid_slab(built, ch, bad, where):
+def test_duplex_invalid_profile_mid_slab(built, ch, bad, where, route, monkeypatch):
     """A gain nibble >= 5 inside slab 2 (mid), in slab 0 (first), on the
     first eblock of slab 3 (boundary: slab 2 copied whole, nothing of slab
     3) or on the stream's last eblock (last): EPROTO, the eblocks before it
     in dst and nothing after it, and the carried state the reference's
-    partial update (continuing with the block fixed equals the oracle)."""
+    partial update (continuing with the block fixed equals the oracle).
+    Direct: the copy-out kernels cut the PCM on the device (the failing
+    slab's status, then a stop word for the slabs after it); staging: the
+    host copies stop there."""
+    route_env(monkeypatch, route)
     bits = 8
     se = slab_eblocks(ch)
     eb = 5 * se + 100
@@ -251,3 +268,30 @@ def test_duplex_shared_input_pages(built):
                     for k in (0, 1, 0, 1)])
     for k, g in zip((0, 1, 0, 1), got):
         assert np.array_equal(g.view(np.int16), refs[k])
+
+
+@pytest.mark.parametrize("case", ["fresh", "unaligned"])
+def test_duplex_output_placement(built, case):
+    """Outputs the direct route does not take: a freshly allocated buffer
+    whose pages were never touched (registering it would fault them all in
+    inside the call; xa_gpu.hip resident()) and one at a 2-byte offset (the
+    copy-out stores 16 B); both go through staging, bit-exact, nothing
+    written past the frames."""
+    eb = 4 * slab_eblocks(2) + 321
+    frames = eb * 32 - 5
+    xa = synth.stream(eb, 8, 2, "A", seed=49)
+    ref, _, _, _ = oracle.decode(xa, eb, 8, 2, (0, 0, 0, 0), frames)
+    n = frames * 2 * 2
+    if case == "fresh":
+        dst = np.empty(eb * 128, np.uint8)
+    else:
+        big = np.full(eb * 128 + 64, 0x5A, np.uint8)
+        dst = big[2:2 + eb * 128]
+        assert dst.ctypes.data % 16 != 0
+    hdr = bjxa_amd.xa_header(xa.size, frames, 44100, 8, 2)
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(hdr)
+        assert d.decode(dst, xa) == eb
+    assert np.array_equal(dst[:n].view(np.int16), ref)
+    if case == "unaligned":
+        assert (big[:2] == 0x5A).all() and (big[2 + n:] == 0x5A).all()

@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--passes", type=int, default=5)
     ap.add_argument("--encode", action="store_true",
                     help="bjxa_encode() of the same stream's PCM instead")
+    ap.add_argument("--fresh", action="store_true",
+                    help="with --alt-env: a new, untouched output buffer for every call "
+                         "(its page faults inside the call, as for a caller that "
+                         "allocates per file)")
     ap.add_argument("--alt-env", default=None,
                     help="NAME=V1,V2: alternate this environment variable between "
                          "calls (a knob the library reads per call) and report the "
@@ -75,20 +79,30 @@ def alt_rate(args):
     bits = 8
     xa = synth.stream(eb, bits, ch, "A", seed=7)
     hdr = bjxa_amd.xa_header(len(xa), eb * 32, 44100, bits, ch)
+    import oracle
+    ref = oracle.decode(xa, eb, bits, ch)[0]
     dst = np.zeros(eb * 64 * ch, dtype=np.uint8)
     times = {v: [] for v in vals}
+    exact = {v: True for v in vals}
     with bjxa_amd.Decoder() as d:
         for i in range(args.passes + 1):
             for v in vals:
                 os.environ[name] = v
+                if args.fresh:
+                    dst = np.empty(eb * 64 * ch, dtype=np.uint8)
+                else:
+                    dst.fill(0)
                 d.parse_header(hdr)
                 t = time.perf_counter()
                 assert d.decode(dst, xa) == eb
                 if i:
                     times[v].append(time.perf_counter() - t)
+                exact[v] = exact[v] and bool(np.array_equal(dst.view(np.int16), ref))
     print(json.dumps({"api": "bjxa_decode (host buffers)", "channels": ch, "eblocks": eb,
-                      "knob": name, "ms_median": {v: round(float(np.median(t)) * 1e3, 3)
-                                                  for v, t in times.items()},
+                      "fresh_output": args.fresh, "knob": name,
+                      "ms_median": {v: round(float(np.median(t)) * 1e3, 3)
+                                    for v, t in times.items()},
+                      "bit_exact": exact,
                       "ms_all": {v: [round(x * 1e3, 3) for x in t] for v, t in times.items()}}))
 
 
