@@ -1397,6 +1397,11 @@ struct reg_hold {
 				break;
 			reg_cv.wait(l);
 		}
+		/* (list nodes allocated up front: nothing below throws while an
+		 * entry is half made, which would leave others waiting on it) */
+		std::list<host_reg> fresh;
+		for (unsigned i = 0; i < nr; i++)
+			fresh.push_back(host_reg{ r[i][0], r[i][1], 1u, true, false });
 		for (unsigned i = 0; i < nr; i++) {
 			auto it = regs.begin();
 			while (it != regs.end() && !(it->a <= r[i][0] && r[i][1] <= it->b))
@@ -1404,8 +1409,14 @@ struct reg_hold {
 			if (it != regs.end()) {
 				it->users++;
 			} else {
-				it = regs.insert(regs.end(), host_reg{ r[i][0], r[i][1], 1u,
-				    true, false });
+				auto f = fresh.begin();
+				for (unsigned j = 0; j < i; j++)
+					if (!mine[j])
+						++f;
+				/* (the node for range i: fresh keeps the unused ones in
+				 * order, so skip those of earlier shared ranges) */
+				it = f;
+				regs.splice(regs.end(), fresh, f);
 				mine[i] = true;
 			}
 			e[n++] = it;
