@@ -840,6 +840,9 @@ struct bjxa__gpu {
 	uint8_t		*h_stage;	/* pinned: DUPLEX_SLOTS staging slots */
 	uint8_t		*d_stage;	/* its device view */
 	uint32_t	*d_sst;		/* per-slab status words */
+	uint32_t	*h_hst;		/* pinned: per-slab status for the host
+					 * (direct route) */
+	uint32_t	*d_hst;		/* its device view */
 	size_t		sst_cap;	/* in slabs */
 };
 
@@ -928,6 +931,8 @@ bjxa__gpu_free(struct bjxa__gpu *g)
 	if (g->h_stage != NULL)
 		(void)hipHostFree(g->h_stage);
 	(void)hipFree(g->d_sst);
+	if (g->h_hst != NULL)
+		(void)hipHostFree(g->h_hst);
 	(void)hipStreamDestroy(g->stream);
 	free(g);
 }
@@ -1133,18 +1138,22 @@ xa_slab_out(const uint4 *src, uint4 *dst, uint64_t n16, const uint32_t *st,
 __global__ __launch_bounds__(256) void
 xa_slab_direct(const uint4 *src, uint8_t *dst, uint64_t nbytes,
     const uint32_t *st, uint32_t *st_out, const uint32_t *stop_prev,
-    uint32_t *stop_cur, uint32_t ob, uint32_t ch)
+    uint32_t *stop_cur, uint32_t ob, uint32_t ch, uint32_t eb_off,
+    uint32_t ek)
 {
+	/* st: the status of the decode holding this slab at eblock eb_off */
 	const uint32_t err = st[XA_ST_ERR];
+	const uint32_t errb = err / ch;
+	const bool failed = err != 0xffffffffu && errb < eb_off + ek;
 	const bool stopped = stop_prev != nullptr && *stop_prev != 0u;
 	if (blockIdx.x == 0 && threadIdx.x < XA_ST_WORDS)
 		st_out[threadIdx.x] = st[threadIdx.x];
 	if (blockIdx.x == 0 && threadIdx.x == 0)
-		*stop_cur = stopped || err != 0xffffffffu ? 1u : 0u;
+		*stop_cur = stopped || failed ? 1u : 0u;
 	if (stopped)
 		return;
-	if (err != 0xffffffffu)
-		nbytes = min(nbytes, (uint64_t)(err / ch) * ob);
+	if (failed)
+		nbytes = errb > eb_off ? min(nbytes, (uint64_t)(errb - eb_off) * ob) : 0u;
 	const uint64_t n16 = nbytes / 16u;
 	uint4 *d = (uint4 *)dst;
 	const uint64_t step = (uint64_t)gridDim.x * 256u * SLAB_OUT_U;
@@ -1198,6 +1207,25 @@ resident(const void *p, size_t len)
 			return false;
 	}
 	return true;
+}
+
+/*
+ * Slabs per decode launch, at most (BJXA_DUPLEX_GROUP, read per call).  A
+ * kernel storing into host memory slows every kernel that writes HBM ~20x
+ * (tools/clog_probe.hip), so a slab decode runs in the gap between two
+ * copy-outs, not beside them; fewer, larger decodes leave fewer gaps.
+ * In-process A/B, groups growing 1, 2, 3, 4 (R6-7): a cap of 1 / 4 / 6 /
+ * 9 / 16 gave 6.15 / 5.66 / 5.70 / 5.69 / 5.70 ms stereo, 5.92 / 5.62 /
+ * 5.67 / 5.66 / 5.65 mono.
+ */
+#define DUPLEX_GROUP	4
+
+static size_t
+duplex_group(void)
+{
+	const char *e = getenv("BJXA_DUPLEX_GROUP");
+	const long v = e != NULL ? strtol(e, NULL, 10) : DUPLEX_GROUP;
+	return v < 1 ? 1u : v > 16 ? (size_t)16 : (size_t)v;
 }
 
 /* BJXA_DUPLEX_DIRECT=0: decodes always copy out through staging (read per
@@ -1299,10 +1327,26 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 		}
 	}
 	if (g->sst_cap < nslab) {
-		/* per slab its status words, then per slab a stop word */
+		/* per slab its status words, then per slab a stop word; and the
+		 * host's copy of the status words */
 		(void)hipFree(g->d_sst);
 		g->d_sst = NULL;
+		if (g->h_hst != NULL)
+			(void)hipHostFree(g->h_hst);
+		g->h_hst = g->d_hst = NULL;
 		g->sst_cap = 0;
+		if (hipHostMalloc((void **)&g->h_hst, nslab * XA_ST_WORDS * 4,
+		    hipHostMallocDefault) != hipSuccess) {
+			g->h_hst = NULL;
+			errno = ENOMEM;
+			return -1;
+		}
+		if (hipHostGetDevicePointer((void **)&g->d_hst, g->h_hst, 0) !=
+		    hipSuccess) {
+			(void)hipHostFree(g->h_hst);
+			g->h_hst = NULL;
+			return io_fail();
+		}
 		if (hipMalloc((void **)&g->d_sst, nslab * (XA_ST_WORDS + 1) * 4) !=
 		    hipSuccess) {
 			g->d_sst = NULL;
@@ -1483,6 +1527,14 @@ duplex_trace(void)
 	return on;
 }
 
+/* staging slot of slab k: its device view, or the host's */
+static uint8_t *
+duplex_slot(const struct bjxa__gpu *g, size_t k, bool device)
+{
+	return (device ? g->d_stage : g->h_stage) + (k % DUPLEX_SLOTS) *
+	    (DUPLEX_HDR + DUPLEX_SLAB);
+}
+
 /*
  * One duplex call over n slabs (decode or encode).  Per slab, on the
  * decode stream: its input H2D, then its kernel; on the copy-out stream,
@@ -1498,14 +1550,19 @@ duplex_trace(void)
  * pinned or registered, say) the copies stay pageable.  With `out`
  * (out_bytes), the caller's output is registered too, and where that works
  * *d_direct is its device view, which the copy-out then writes instead of
- * staging (else NULL).  Calls whose buffers share pages share or wait for
- * each other's registrations (reg_hold).
+ * staging; where it cannot be registered, -2 before anything is
+ * enqueued.  Calls whose buffers share pages share or wait for each
+ * other's registrations (reg_hold).
  *   in_range(k, &off, &len)    slab k's input bytes [off, off + len)
- *   gpu(k, slot, ev, sd)       enqueue slab k's kernel on sd (the decode
+ *   gpu(k, ev, sd, ev_out)     enqueue slab k's kernel on sd (the decode
  *                              stream, after its input), record ev there,
  *                              and its copy-out (into the device view of
- *                              staging slot `slot`, or *d_direct) on
- *                              g->s_out after ev; false on failure
+ *                              its staging slot, duplex_slot(), or
+ *                              *d_direct) on g->s_out after ev, recording
+ *                              ev_out[k] after it; a decode may hold back
+ *                              a slab's kernel and copy-out to run them
+ *                              with a later slab's (at most DUPLEX_SLOTS - 1
+ *                              later); false on failure
  *   host(k, slot)              the calling thread's part once slab k's
  *                              copy-out is done: copy it out of its slot
  *                              (staging) or check its status; returns 1
@@ -1559,6 +1616,8 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 			*d_direct = NULL;
 		}
 	}
+	if (out != NULL && *d_direct == NULL)
+		return -2;	/* nothing enqueued: the caller goes on without out */
 	uint8_t *d_in = (uint8_t *)g->d_in;
 	auto issue = [&](size_t k) -> bool {
 		size_t off, len;
@@ -1568,18 +1627,19 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 			return false;
 		if (tr)
 			t_in[k] = trace_ms() - t0;
-		uint8_t *slot = g->d_stage + (k % DUPLEX_SLOTS) *
-		    (DUPLEX_HDR + DUPLEX_SLAB);
-		if (!gpu(k, slot, ev_dec[k], g->s_dec) ||
-		    hipEventRecord(ev_out[k], g->s_out) != hipSuccess)
+		if (!gpu(k, ev_dec[k], g->s_dec, ev_out))
 			return false;
 		if (tr)
 			t_iss[k] = trace_ms() - t0;
 		return true;
 	};
 
+	/* slabs in flight: as many as staging slots, or every slab when the
+	 * output is written directly (the host then reads only status words,
+	 * g->h_hst) */
+	const size_t depth = *d_direct != NULL ? n : (size_t)DUPLEX_SLOTS;
 	bool ok = true;
-	for (size_t k = 0; ok && k < std::min(n, (size_t)DUPLEX_SLOTS); k++)
+	for (size_t k = 0; ok && k < std::min(n, depth); k++)
 		ok = issue(k);
 	for (size_t k = 0; ok && k < n; k++) {
 		if (hipEventSynchronize(ev_out[k]) != hipSuccess) {
@@ -1588,16 +1648,17 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 		}
 		if (tr)
 			t_out[k] = trace_ms() - t0;
-		const int r = host(k, g->h_stage + (k % DUPLEX_SLOTS) *
-		    (DUPLEX_HDR + DUPLEX_SLAB));
+		const int r = host(k, *d_direct != NULL ?
+		    (const uint8_t *)(g->h_hst + k * XA_ST_WORDS) :
+		    duplex_slot(g, k, false));
 		if (tr)
 			t_cp[k] = trace_ms() - t0;
 		if (r <= 0) {
 			ok = r == 0;
 			break;
 		}
-		if (k + DUPLEX_SLOTS < n)
-			ok = issue(k + DUPLEX_SLOTS);
+		if (k + depth < n)
+			ok = issue(k + depth);
 	}
 	/* everything enqueued has to finish before the buffers are reused */
 	const bool synced = hipStreamSynchronize(g->s_dec) == hipSuccess &&
@@ -1619,7 +1680,25 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 	const size_t ebsz = (size_t)(bits * 4 + 1) * ch, ob = 64u * ch;
 	const uint32_t se = (uint32_t)(DUPLEX_SLAB / ob);	/* eblocks per slab */
 	const size_t n = (eblocks + (size_t)se - 1) / se;
-	if (duplex_setup(g, n) < 0 || call_buffers(g, eblocks, se, bits, ch) < 0)
+	/* decode groups: slab 0 alone (the first output as early as possible),
+	 * then 2, 3, 4, 6, 9 ... up to gmax slabs per decode launch */
+	const size_t gmax = duplex_group();
+	std::vector<size_t> first(n);
+	auto plan = [&](size_t gm) {
+		for (size_t k = 0, a = 0, len = 1; k < n; k++) {
+			if (k == a + len) {
+				/* a group's input (~0.2 ms a slab beside the
+				 * copy-outs) has to land within the previous
+				 * group's copy-outs (~0.33 ms a slab): grow by half */
+				a = k;
+				len = std::min(std::max(len + 1, 3 * len / 2), gm);
+			}
+			first[k] = a;
+		}
+	};
+	auto last = [&](size_t k) { return k + 1 == n || first[k + 1] != first[k]; };
+	if (duplex_setup(g, n) < 0 || call_buffers(g, eblocks,
+	    (uint32_t)std::min((uint64_t)eblocks, (uint64_t)gmax * se), bits, ch) < 0)
 		return -1;
 	/* (a workspace initialised on g->stream, used on g->s_dec) */
 	if (hipStreamSynchronize(g->stream) != hipSuccess)
@@ -1632,71 +1711,98 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 	/* the PCM straight into the caller's buffer where it can be registered,
 	 * is 16-B aligned (the copy-out's stores) and is already in memory;
 	 * else through staging */
-	const bool direct = duplex_direct() && ((uintptr_t)dst & 15u) == 0 &&
+	bool direct = duplex_direct() && ((uintptr_t)dst & 15u) == 0 &&
 	    resident(dst, (size_t)dst_bytes);
 	uint32_t *stop = g->d_sst + g->sst_cap * XA_ST_WORDS;
 	uint8_t *d_dir = NULL;
-	const int r = duplex_run(g, n, src, (size_t)eblocks * ebsz,
+	int r;
+	/* (direct: every slab in flight, so any group size; staging: a group
+	 * must fit the DUPLEX_SLOTS slabs in flight.  Where the output cannot
+	 * be registered after all, duplex_run returns -2 before enqueueing
+	 * anything, and the call goes through staging) */
+again:
+	plan(direct ? gmax : std::min(gmax, (size_t)DUPLEX_SLOTS));
+	r = duplex_run(g, n, src, (size_t)eblocks * ebsz,
 	    direct ? dst : NULL, (size_t)dst_bytes, &d_dir,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ebsz;
 		*len = slab_eb(k) * ebsz;
-	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done, hipStream_t sd) -> bool {
-		const uint32_t e0 = (uint32_t)(k * se), ek = slab_eb(k);
+	}, [&](size_t k, hipEvent_t ev_done, hipStream_t sd, hipEvent_t *ev_out) -> bool {
+		if (!last(k))
+			return true;	/* with the group's last slab */
+		const size_t a = first[k];
+		const uint32_t e0 = (uint32_t)(a * se);
+		const uint32_t eg = (uint32_t)(k * se + slab_eb(k)) - e0;
 		bjxa_hip_stream_t s;
 		memset(&s, 0, sizeof s);
 		s.d_src = (uint8_t *)g->d_in + (size_t)e0 * ebsz;
 		s.d_dst = (uint8_t *)g->d_out + (size_t)e0 * ob;
-		s.eblocks = ek;
-		s.frames = (uint64_t)ek * 32u;
+		s.eblocks = eg;
+		s.frames = (uint64_t)eg * 32u;
 		s.bits = (uint8_t)bits;
 		s.channels = (uint8_t)ch;
 		memcpy(s.state, state, sizeof s.state);
+		/* the group's status sits at its last slab, its entry state at the
+		 * previous group's */
 		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
 		if (decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, sd,
-		    k > 0 ? sst - XA_ST_WORDS : NULL) < 0 ||
+		    a > 0 ? g->d_sst + (a - 1) * XA_ST_WORDS : NULL) < 0 ||
 		    hipEventRecord(ev_done, sd) != hipSuccess ||
 		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
 			return false;
-		if (d_dir != NULL) {
-			const size_t lo = (size_t)e0 * ob;
-			const size_t hi = std::min((size_t)dst_bytes, lo + (size_t)ek * ob);
-			hipLaunchKernelGGL(xa_slab_direct, dim3(2 * DUPLEX_OUT_CUS),
-			    dim3(256), 0, g->s_out, (const uint4 *)s.d_dst, d_dir + lo,
-			    (uint64_t)(hi > lo ? hi - lo : 0), sst, (uint32_t *)slot,
-			    k > 0 ? stop + k - 1 : (const uint32_t *)NULL, stop + k,
-			    (uint32_t)ob, (uint32_t)ch);
-		} else {
-			hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS),
-			    dim3(256), 0, g->s_out, (const uint4 *)s.d_dst,
-			    (uint4 *)(slot + DUPLEX_HDR), (uint64_t)ek * ob / 16u, sst,
-			    (uint32_t *)slot);
+		for (size_t j = a; j <= k; j++) {
+			const uint32_t ej = slab_eb(j);
+			const uint8_t *pj = (const uint8_t *)g->d_out + j * se * ob;
+			uint8_t *slot = duplex_slot(g, j, true);
+			if (d_dir != NULL) {
+				const size_t lo = j * se * ob;
+				const size_t hi = std::min((size_t)dst_bytes,
+				    lo + (size_t)ej * ob);
+				hipLaunchKernelGGL(xa_slab_direct, dim3(2 * DUPLEX_OUT_CUS),
+				    dim3(256), 0, g->s_out, (const uint4 *)pj, d_dir + lo,
+				    (uint64_t)(hi > lo ? hi - lo : 0), sst,
+				    g->d_hst + j * XA_ST_WORDS,
+				    j > 0 ? stop + j - 1 : (const uint32_t *)NULL, stop + j,
+				    (uint32_t)ob, (uint32_t)ch, (uint32_t)((j - a) * se), ej);
+			} else {
+				hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS),
+				    dim3(256), 0, g->s_out, (const uint4 *)pj,
+				    (uint4 *)(slot + DUPLEX_HDR), (uint64_t)ej * ob / 16u, sst,
+				    (uint32_t *)slot);
+			}
+			if (hipGetLastError() != hipSuccess ||
+			    hipEventRecord(ev_out[j], g->s_out) != hipSuccess)
+				return false;
 		}
-		return hipGetLastError() == hipSuccess;
+		return true;
 	}, [&](size_t k, const uint8_t *slot) -> int {
 		uint32_t st[XA_ST_WORDS];
 		memcpy(st, (const void *)slot, sizeof st);
-		if (d_dir != NULL) {	/* the kernel wrote the PCM, and cut it */
-			if (st[XA_ST_ERR] != 0xffffffffu) {
-				err = (uint32_t)(k * se * ch) + st[XA_ST_ERR];
-				return 0;
-			}
-			memcpy(fin, st, sizeof fin);
-			return 1;
-		}
-		const size_t lo = k * se * ob;
-		size_t hi = std::min((size_t)dst_bytes, (k * se + slab_eb(k)) * ob);
-		if (st[XA_ST_ERR] != 0xffffffffu) {
-			err = (uint32_t)(k * se * ch) + st[XA_ST_ERR];
-			hi = std::min(hi, (size_t)(err / ch) * ob);
-		}
-		if (hi > lo)
-			duplex_copy(dst + lo, slot + DUPLEX_HDR, hi - lo);
-		if (err != 0xffffffffu)
+		/* the status is its decode group's: a failing block in this slab
+		 * stops here, one in a later slab of the group later */
+		const size_t a = first[k];
+		const bool failed = st[XA_ST_ERR] != 0xffffffffu &&
+		    a * se + st[XA_ST_ERR] / ch < k * se + slab_eb(k);
+		if (failed)
+			err = (uint32_t)(a * se * ch) + st[XA_ST_ERR];
+		if (d_dir == NULL) {
+			const size_t lo = k * se * ob;
+			size_t hi = std::min((size_t)dst_bytes, (k * se + slab_eb(k)) * ob);
+			if (failed)
+				hi = std::min(hi, (size_t)(err / ch) * ob);
+			if (hi > lo)
+				duplex_copy(dst + lo, slot + DUPLEX_HDR, hi - lo);
+		}	/* (direct: the copy-out kernel wrote the PCM, and cut it) */
+		if (failed)
 			return 0;
-		memcpy(fin, st, sizeof fin);
+		if (last(k))
+			memcpy(fin, st, sizeof fin);
 		return 1;
 	});
+	if (r == -2 && direct) {
+		direct = false;
+		goto again;
+	}
 	if (r < 0)
 		return -1;
 	g->ws_stale = false;
@@ -1735,7 +1841,8 @@ duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ib;
 		*len = (size_t)slab_frames(k) * 2u * ch;
-	}, [&](size_t k, uint8_t *slot, hipEvent_t ev_done, hipStream_t sd) -> bool {
+	}, [&](size_t k, hipEvent_t ev_done, hipStream_t sd, hipEvent_t *ev_out) -> bool {
+		uint8_t *slot = duplex_slot(g, k, true);
 		const uint64_t fk = slab_frames(k);
 		const size_t xk = (size_t)((fk + 31) / 32) * ebsz;
 		uint8_t *d_xa = (uint8_t *)g->d_out + k * se * ebsz;
@@ -1748,7 +1855,8 @@ duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
 		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256),
 		    0, g->s_out, (const uint4 *)d_xa, (uint4 *)(slot + DUPLEX_HDR),
 		    (uint64_t)((xk + 15) / 16), g->d_sst, (uint32_t *)slot);
-		return hipGetLastError() == hipSuccess;
+		return hipGetLastError() == hipSuccess &&
+		    hipEventRecord(ev_out[k], g->s_out) == hipSuccess;
 	}, [&](size_t k, const uint8_t *slot) -> int {
 		const size_t xk = (size_t)((slab_frames(k) + 31) / 32) * ebsz;
 		duplex_copy(dst + k * se * ebsz, slot + DUPLEX_HDR, xk);
