@@ -1228,6 +1228,42 @@ duplex_group(void)
 	return v < 1 ? 1u : v > 16 ? (size_t)16 : (size_t)v;
 }
 
+/*
+ * Slabs per encode launch, at most (BJXA_DUPLEX_EGROUP, read per call).  The
+ * encode's long direction is its input, which runs back to back on the copy
+ * engine once the XA goes straight into the caller's buffer; grouping then
+ * only lengthens the last group's copy-outs after the input ends (cap 1 / 4
+ * / 8 / 16: 5.79 / 5.88 / 6.24 / 6.24 ms stereo, R6-7), so one slab a launch.
+ */
+#define DUPLEX_EGROUP	1
+
+static size_t
+duplex_egroup(void)
+{
+	const char *e = getenv("BJXA_DUPLEX_EGROUP");
+	const long v = e != NULL ? strtol(e, NULL, 10) : DUPLEX_EGROUP;
+	return v < 1 ? 1u : v > 16 ? (size_t)16 : (size_t)v;
+}
+
+/*
+ * Groups of slabs per kernel launch: first[k] = the first slab of k's
+ * group.  Slab 0 alone (the first output as early as possible), then groups
+ * growing by half up to gm: a group's input (~0.2 ms a slab beside the
+ * copy-outs) has to land within the previous group's copy-outs (~0.33 ms a
+ * slab).
+ */
+static void
+duplex_groups(std::vector<size_t> &first, size_t gm)
+{
+	for (size_t k = 0, a = 0, len = 1; k < first.size(); k++) {
+		if (k == a + len) {
+			a = k;
+			len = std::min(std::max(len + 1, 3 * len / 2), gm);
+		}
+		first[k] = a;
+	}
+}
+
 /* BJXA_DUPLEX_DIRECT=0: decodes always copy out through staging (read per
  * call, so one process can A/B it) */
 static bool
@@ -1680,22 +1716,10 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 	const size_t ebsz = (size_t)(bits * 4 + 1) * ch, ob = 64u * ch;
 	const uint32_t se = (uint32_t)(DUPLEX_SLAB / ob);	/* eblocks per slab */
 	const size_t n = (eblocks + (size_t)se - 1) / se;
-	/* decode groups: slab 0 alone (the first output as early as possible),
-	 * then 2, 3, 4, 6, 9 ... up to gmax slabs per decode launch */
+	/* decode groups (duplex_groups): 1, 2, 3, 4 ... up to gmax slabs */
 	const size_t gmax = duplex_group();
 	std::vector<size_t> first(n);
-	auto plan = [&](size_t gm) {
-		for (size_t k = 0, a = 0, len = 1; k < n; k++) {
-			if (k == a + len) {
-				/* a group's input (~0.2 ms a slab beside the
-				 * copy-outs) has to land within the previous
-				 * group's copy-outs (~0.33 ms a slab): grow by half */
-				a = k;
-				len = std::min(std::max(len + 1, 3 * len / 2), gm);
-			}
-			first[k] = a;
-		}
-	};
+	auto plan = [&](size_t gm) { duplex_groups(first, gm); };
 	auto last = [&](size_t k) { return k + 1 == n || first[k + 1] != first[k]; };
 	if (duplex_setup(g, n) < 0 || call_buffers(g, eblocks,
 	    (uint32_t)std::min((uint64_t)eblocks, (uint64_t)gmax * se), bits, ch) < 0)
@@ -1816,8 +1840,10 @@ again:
 /*
  * The same route for a large encode: PCM slabs in on the copy engine (the
  * long direction, 256 MB for a 2M-eblock stereo call), the encode kernel
- * per slab, and its XA (132 MB) streamed to pinned staging by the copy
- * kernel.  Slabs are independent (the encoder keeps no state, :665-691).
+ * per slab, and its XA (132 MB) streamed by the copy kernel straight into
+ * the caller's buffer when it can be registered (every slab in flight, the
+ * input back to back), else into pinned staging.  Slabs are independent
+ * (the encoder keeps no state, :665-691).
  */
 static int
 duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
@@ -1836,32 +1862,77 @@ duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
 		return std::min((uint64_t)frames - (uint64_t)k * se * 32u,
 		    (uint64_t)se * 32u);
 	};
-	uint8_t *d_dir = NULL;	/* (XA through staging: not the long direction) */
-	return duplex_run(g, n, src, in_bytes, NULL, 0, &d_dir,
+	/* encode groups, as the decode's (through staging: bounded by the
+	 * staging slots) */
+	const size_t xa_bytes = (size_t)eblocks * ebsz;
+	bool direct = duplex_direct() && ((uintptr_t)dst & 15u) == 0 &&
+	    resident(dst, xa_bytes);
+	std::vector<size_t> first(n);
+	auto last = [&](size_t k) { return k + 1 == n || first[k + 1] != first[k]; };
+	uint8_t *d_dir = NULL;
+	uint32_t *stop = g->d_sst + g->sst_cap * XA_ST_WORDS;
+	/* (the direct copy-out reads a status: one that reports no failure) */
+	if (direct && hipMemsetAsync(g->d_sst, 0xff, XA_ST_WORDS * 4, g->s_dec) !=
+	    hipSuccess)
+		return io_fail();
+	int r;
+again:
+	duplex_groups(first, direct ? duplex_egroup() :
+	    std::min(duplex_egroup(), (size_t)DUPLEX_SLOTS));
+	r = duplex_run(g, n, src, in_bytes, direct ? dst : NULL, xa_bytes, &d_dir,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ib;
 		*len = (size_t)slab_frames(k) * 2u * ch;
 	}, [&](size_t k, hipEvent_t ev_done, hipStream_t sd, hipEvent_t *ev_out) -> bool {
-		uint8_t *slot = duplex_slot(g, k, true);
-		const uint64_t fk = slab_frames(k);
-		const size_t xk = (size_t)((fk + 31) / 32) * ebsz;
-		uint8_t *d_xa = (uint8_t *)g->d_out + k * se * ebsz;
-		if (bjxa_hip_encode_async((uint8_t *)g->d_in + k * se * ib, fk, bits,
-		    ch, d_xa, sd) < 0 ||
+		if (!last(k))
+			return true;	/* with the group's last slab */
+		const size_t a = first[k];
+		uint64_t fg = 0;
+		for (size_t j = a; j <= k; j++)
+			fg += slab_frames(j);
+		if (bjxa_hip_encode_async((uint8_t *)g->d_in + a * se * ib, fg, bits,
+		    ch, (uint8_t *)g->d_out + a * se * ebsz, sd) < 0 ||
 		    hipEventRecord(ev_done, sd) != hipSuccess ||
 		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
 			return false;
-		/* whole 16-B pieces (the slot has room past the slab's XA) */
-		hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS), dim3(256),
-		    0, g->s_out, (const uint4 *)d_xa, (uint4 *)(slot + DUPLEX_HDR),
-		    (uint64_t)((xk + 15) / 16), g->d_sst, (uint32_t *)slot);
-		return hipGetLastError() == hipSuccess &&
-		    hipEventRecord(ev_out[k], g->s_out) == hipSuccess;
+		for (size_t j = a; j <= k; j++) {
+			uint8_t *slot = duplex_slot(g, j, true);
+			const size_t xk = (size_t)((slab_frames(j) + 31) / 32) * ebsz;
+			const uint4 *pj = (const uint4 *)((uint8_t *)g->d_out +
+			    j * se * ebsz);
+			if (d_dir != NULL) {
+				/* exact bytes into the caller's buffer */
+				hipLaunchKernelGGL(xa_slab_direct, dim3(2 * DUPLEX_OUT_CUS),
+				    dim3(256), 0, g->s_out, pj, d_dir + j * se * ebsz,
+				    (uint64_t)xk, (const uint32_t *)g->d_sst,
+				    g->d_hst + j * XA_ST_WORDS,
+				    j > 0 ? stop + j - 1 : (const uint32_t *)NULL, stop + j,
+				    (uint32_t)ebsz, (uint32_t)ch, 0u, 1u);
+			} else {
+				/* whole 16-B pieces (the slot has room past the
+				 * slab's XA) */
+				hipLaunchKernelGGL(xa_slab_out, dim3(2 * DUPLEX_OUT_CUS),
+				    dim3(256), 0, g->s_out, pj,
+				    (uint4 *)(slot + DUPLEX_HDR), (uint64_t)((xk + 15) / 16),
+				    g->d_sst, (uint32_t *)slot);
+			}
+			if (hipGetLastError() != hipSuccess ||
+			    hipEventRecord(ev_out[j], g->s_out) != hipSuccess)
+				return false;
+		}
+		return true;
 	}, [&](size_t k, const uint8_t *slot) -> int {
+		if (d_dir != NULL)
+			return 1;	/* (the copy-out kernel wrote the XA) */
 		const size_t xk = (size_t)((slab_frames(k) + 31) / 32) * ebsz;
 		duplex_copy(dst + k * se * ebsz, slot + DUPLEX_HDR, xk);
 		return 1;
 	});
+	if (r == -2 && direct) {
+		direct = false;
+		goto again;
+	}
+	return r;
 }
 
 extern "C" int

@@ -169,18 +169,25 @@ def host_encode(pcm, frames, bits, ch):
         fmt = e.init({"data_len_pcm": frames * 2 * ch, "blocks": 0, "block_size_pcm": 0,
                       "block_size_xa": 0, "samples_rate": 44100, "sample_bits": 16,
                       "channels": ch}, bits)
-        dst = np.full(fmt["blocks"] * fmt["block_size_xa"], 0xA5, np.uint8)
+        n = fmt["blocks"] * fmt["block_size_xa"]
+        buf = np.full(n + 64, 0xA5, np.uint8)      # a guard past the XA
+        dst = buf[:n]
         assert e.encode(dst, pcm.view(np.uint8)) == fmt["blocks"]
+        assert (buf[n:] == 0xA5).all()
     finally:
         e.close()
     return dst
 
 
+@pytest.mark.parametrize("route", ROUTES)
 @pytest.mark.parametrize("bits,ch", [(8, 2), (4, 1), (6, 2), (4, 2)])
-def test_duplex_encode_matches_oracle(built, bits, ch):
+def test_duplex_encode_matches_oracle(built, bits, ch, route, monkeypatch):
     """The encode side of the route (xa_gpu.hip duplex_encode): PCM slabs
-    in on the copy engine, XA out through staging; five slabs and a ragged
-    sixth whose last block is zero-padded (src/libbjxa.c:686-690)."""
+    in on the copy engine, XA out straight into the registered caller
+    buffer (direct) or through staging; five slabs and a ragged sixth whose
+    last block is zero-padded (src/libbjxa.c:686-690), nothing written past
+    the XA."""
+    route_env(monkeypatch, route)
     eb = 5 * slab_eblocks(ch) + 4321
     frames = eb * 32 - 9
     pcm = synth.pcm(frames, ch, seed=50 + bits + ch)

@@ -39,6 +39,8 @@ def main():
                          "calls (a knob the library reads per call) and report the "
                          "median per value")
     args = ap.parse_args()
+    if args.alt_env and args.encode:
+        return alt_encode_rate(args)
     if args.alt_env:
         return alt_rate(args)
     if args.encode:
@@ -103,6 +105,41 @@ def alt_rate(args):
                       "ms_median": {v: round(float(np.median(t)) * 1e3, 3)
                                     for v, t in times.items()},
                       "bit_exact": exact,
+                      "ms_all": {v: [round(x * 1e3, 3) for x in t] for v, t in times.items()}}))
+
+
+def alt_encode_rate(args):
+    """bjxa_encode() calls alternating a per-call library knob, in one
+    process."""
+    name, vals = args.alt_env.split("=", 1)
+    vals = vals.split(",")
+    ch = args.ch
+    eb = 2_000_000 if ch == 2 else 4_000_000
+    bits, frames = 8, eb * 32
+    pcm = synth.pcm(frames, ch, seed=7)
+    fmt0 = {"data_len_pcm": frames * 2 * ch, "blocks": 0, "block_size_pcm": 0,
+            "block_size_xa": 0, "samples_rate": 44100, "sample_bits": 16, "channels": ch}
+    dst = np.zeros(eb * ch * (bits * 4 + 1), np.uint8)
+    import oracle
+    ref = oracle.encode(pcm, frames, bits, ch)
+    times = {v: [] for v in vals}
+    exact = {v: True for v in vals}
+    e = bjxa_amd.Encoder()
+    for i in range(args.passes + 1):
+        for v in vals:
+            os.environ[name] = v
+            dst.fill(0)
+            e.init(fmt0, bits)
+            t = time.perf_counter()
+            assert e.encode(dst, pcm.view(np.uint8)) == eb
+            if i:
+                times[v].append(time.perf_counter() - t)
+            exact[v] = exact[v] and bool(np.array_equal(dst, ref))
+    e.close()
+    print(json.dumps({"api": "bjxa_encode (host buffers)", "channels": ch, "eblocks": eb,
+                      "knob": name, "ms_median": {v: round(float(np.median(t)) * 1e3, 3)
+                                                  for v, t in times.items()},
+                      "byte_exact": exact,
                       "ms_all": {v: [round(x * 1e3, 3) for x in t] for v, t in times.items()}}))
 
 
