@@ -1087,10 +1087,13 @@ call_buffers(struct bjxa__gpu *g, uint32_t eblocks, uint32_t ws_eblocks,
  * route does; nothing is written to dst past it.  BJXA_DUPLEX=0 (read at
  * the first call) keeps every call on the serial route.
  */
-#define DUPLEX_SLAB		((size_t)16 << 20)	/* PCM bytes per slab */
+#ifndef DUPLEX_SLAB_MIB
+#define DUPLEX_SLAB_MIB		16
+#endif
+#define DUPLEX_SLAB		((size_t)DUPLEX_SLAB_MIB << 20)	/* PCM bytes per slab */
 #define DUPLEX_SLOTS		4
 #define DUPLEX_HDR		4096			/* status, then the slab */
-#define DUPLEX_MIN_SLABS	4
+#define DUPLEX_MIN_SLABS	(64 / DUPLEX_SLAB_MIB)	/* calls of >= 64 MiB of PCM */
 #define DUPLEX_OUT_CUS		64	/* the copy-out stream's CUs; 2 workgroups each */
 
 /*
@@ -1218,7 +1221,9 @@ resident(const void *p, size_t len)
  * 9 / 16 gave 6.15 / 5.66 / 5.70 / 5.69 / 5.70 ms stereo, 5.92 / 5.62 /
  * 5.67 / 5.66 / 5.65 mono.
  */
+#ifndef DUPLEX_GROUP
 #define DUPLEX_GROUP	4
+#endif
 
 static size_t
 duplex_group(void)
