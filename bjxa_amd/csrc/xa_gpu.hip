@@ -844,6 +844,8 @@ struct bjxa__gpu {
 					 * (direct route) */
 	uint32_t	*d_hst;		/* its device view */
 	size_t		sst_cap;	/* in slabs */
+	hipEvent_t	*evp;		/* the route's events, kept across calls */
+	size_t		evp_n;
 };
 
 static int
@@ -933,6 +935,9 @@ bjxa__gpu_free(struct bjxa__gpu *g)
 	(void)hipFree(g->d_sst);
 	if (g->h_hst != NULL)
 		(void)hipHostFree(g->h_hst);
+	for (size_t i = 0; i < g->evp_n; i++)
+		(void)hipEventDestroy(g->evp[i]);
+	free(g->evp);
 	(void)hipStreamDestroy(g->stream);
 	free(g);
 }
@@ -1401,23 +1406,30 @@ duplex_setup(struct bjxa__gpu *g, size_t nslab)
 
 namespace {
 
-/* hipEvents of one duplex call */
-struct event_set {
-	std::vector<hipEvent_t> ev;
-	bool ok = true;
-	explicit event_set(size_t n) : ev(n, NULL)
-	{
-		for (hipEvent_t &e : ev)
-			ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) ==
-			    hipSuccess;
+/* at least n events in g's pool (created once, kept across calls: ~2n
+ * event creations per call cost more than the route's host work) */
+int
+event_pool(struct bjxa__gpu *g, size_t n)
+{
+	if (g->evp_n >= n)
+		return 0;
+	hipEvent_t *p = (hipEvent_t *)realloc(g->evp, n * sizeof *p);
+	if (p == NULL) {
+		errno = ENOMEM;
+		return -1;
 	}
-	~event_set()
-	{
-		for (hipEvent_t e : ev)
-			if (e != NULL)
-				(void)hipEventDestroy(e);
+	g->evp = p;
+	while (g->evp_n < n) {
+		if (hipEventCreateWithFlags(&p[g->evp_n], hipEventDisableTiming) !=
+		    hipSuccess) {
+			(void)hipGetLastError();
+			errno = EIO;
+			return -1;
+		}
+		g->evp_n++;
 	}
-};
+	return 0;
+}
 
 /*
  * The duplex route's registrations of caller memory, process-wide.  A call
@@ -1641,16 +1653,16 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
     uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
     Gpu &&gpu, Host &&host)
 {
-	event_set evs(2 * n);	/* kernel done, copy-out done */
-	if (!evs.ok)
-		return io_fail();
-	hipEvent_t *ev_dec = evs.ev.data(), *ev_out = ev_dec + n;
+	if (event_pool(g, 2 * n) < 0)	/* kernel done, copy-out done */
+		return -1;
+	hipEvent_t *ev_dec = g->evp, *ev_out = ev_dec + n;
 	const bool tr = duplex_trace();
 	std::vector<double> t_in(n, 0.0), t_iss(n, 0.0), t_out(n, 0.0), t_cp(n, 0.0);
 	const double t0 = tr ? trace_ms() : 0.0;
 
 	/* (released on return, after the streams are synchronised) */
 	reg_hold reg(src, in_bytes, out, out_bytes);
+	const double t_reg = tr ? trace_ms() - t0 : 0.0;
 	if (out != NULL && reg.registered(out, out_bytes)) {
 		if (hipHostGetDevicePointer((void **)d_direct, out, 0) != hipSuccess) {
 			(void)hipGetLastError();
@@ -1705,7 +1717,8 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	const bool synced = hipStreamSynchronize(g->s_dec) == hipSuccess &&
 	    hipStreamSynchronize(g->s_out) == hipSuccess;
 	if (tr) {
-		fprintf(stderr, "duplex %zu slabs, done %.3f ms\n", n, trace_ms() - t0);
+		fprintf(stderr, "duplex %zu slabs, registered %.3f ms, done %.3f ms\n",
+		    n, t_reg, trace_ms() - t0);
 		for (size_t k = 0; k < n; k++)
 			fprintf(stderr, "  slab %2zu in %.3f issued %.3f out %.3f copied %.3f\n",
 			    k, t_in[k], t_iss[k], t_out[k], t_cp[k]);
@@ -1950,9 +1963,14 @@ bjxa__gpu_decode(struct bjxa__gpu *g, const void *src, uint32_t eblocks,
 		return small_decode(g, src, eblocks, bits, ch, state, dst,
 		    dst_bytes, err_cb);
 	if (duplex_enabled() && (uint64_t)eblocks * 64u * ch >=
-	    DUPLEX_MIN_SLABS * DUPLEX_SLAB)
-		return duplex_decode(g, (const uint8_t *)src, eblocks, bits, ch,
-		    state, (uint8_t *)dst, dst_bytes, err_cb);
+	    DUPLEX_MIN_SLABS * DUPLEX_SLAB) {
+		const double t0 = duplex_trace() ? trace_ms() : 0.0;
+		const int r = duplex_decode(g, (const uint8_t *)src, eblocks, bits,
+		    ch, state, (uint8_t *)dst, dst_bytes, err_cb);
+		if (duplex_trace())
+			fprintf(stderr, "duplex decode call %.3f ms\n", trace_ms() - t0);
+		return r;
+	}
 
 	const size_t in_bytes = (size_t)(bits * 4 + 1) * ch * eblocks;
 	bjxa_hip_stream_t s;
