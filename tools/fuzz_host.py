@@ -28,10 +28,10 @@ import oracle  # noqa: E402
 from bjxa_amd import synth  # noqa: E402
 
 
-def decode_round(rng, stats):
+def decode_round(rng, stats, max_eb=2_500_000):
     bits = int(rng.choice([4, 6, 8]))
     ch = int(rng.integers(1, 3))
-    eb = max(1, int(np.exp(rng.uniform(0, np.log(2_500_000)))))
+    eb = max(1, int(np.exp(rng.uniform(0, np.log(max_eb)))))
     mix = ["A", "W", "F", "Z"][int(rng.integers(0, 4))]
     bx = (bits * 4 + 1) * ch
     eb = min(eb, ((1 << 27) - 1) // bx)     # one XA header's data_len < 2^27
@@ -83,12 +83,12 @@ def decode_round(rng, stats):
                                      "frames": frames, "bounds": bounds[:6], "bad": badc}
 
 
-def encode_round(rng, stats):
+def encode_round(rng, stats, max_frames=64_000_000):
     bits = int(rng.choice([4, 6, 8]))
     ch = int(rng.integers(1, 3))
     # (at least one block of PCM: the reference's bjxa_encode wants a whole
     # block of source, src/libbjxa.c:778, ENOBUFS below it)
-    frames = max(32, int(np.exp(rng.uniform(np.log(32), np.log(64_000_000 // ch)))))
+    frames = max(32, int(np.exp(rng.uniform(np.log(32), np.log(max_frames // ch)))))
     pcm = synth.pcm(frames, ch, seed=int(rng.integers(0, 1 << 30)))
     e = bjxa_amd.Encoder()
     try:
@@ -111,14 +111,18 @@ def encode_round(rng, stats):
     return None if why is None else {"why": why, "bits": bits, "ch": ch, "frames": frames}
 
 
+def new_stats():
+    return {"decode_streams": 0, "decode_calls": 0, "eblocks": 0, "eproto": 0,
+            "encode_streams": 0, "by_size": {}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
     ap.add_argument("--seed", type=int, default=1)
     args = ap.parse_args()
     rng = np.random.default_rng(args.seed)
-    stats = {"decode_streams": 0, "decode_calls": 0, "eblocks": 0, "eproto": 0,
-             "encode_streams": 0, "by_size": {}}
+    stats = new_stats()
     bad = []
     deadline = time.monotonic() + args.seconds
     while time.monotonic() < deadline:
