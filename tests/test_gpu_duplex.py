@@ -302,3 +302,21 @@ def test_duplex_output_placement(built, case):
     assert np.array_equal(dst[:n].view(np.int16), ref)
     if case == "unaligned":
         assert (big[:2] == 0x5A).all() and (big[2 + n:] == 0x5A).all()
+
+
+def test_duplex_pinned_output(built):
+    """An output buffer that is already pinned: registering it for the
+    direct route fails, the call goes back to staging before anything is
+    enqueued (duplex_run returns -2), same bytes."""
+    import torch
+    eb = 4 * slab_eblocks(2) + 7
+    xa = synth.stream(eb, 8, 2, "A", seed=51)
+    ref, _, _, _ = oracle.decode(xa, eb, 8, 2)
+    pinned = torch.empty(eb * 128, dtype=torch.uint8, pin_memory=True)
+    dst = pinned.numpy()
+    dst[:] = 0x5A
+    hdr = bjxa_amd.xa_header(xa.size, eb * 32, 44100, 8, 2)
+    with bjxa_amd.Decoder() as d:
+        d.parse_header(hdr)
+        assert d.decode(dst, xa) == eb
+    assert np.array_equal(dst.view(np.int16), ref)

@@ -89,7 +89,11 @@ def main():
     stats = {"single": 0, "batch_streams": 0, "batches": 0, "with_bad": 0, "eblocks": 0}
     bad_cases = []
     deadline = time.monotonic() + args.seconds
+    tick = time.monotonic() + 30
     while time.monotonic() < deadline:
+        if time.monotonic() > tick:         # (a progress line every 30 s)
+            tick += 30
+            print("progress", json.dumps(stats), file=sys.stderr, flush=True)
         if rng.random() < 0.5:
             s = draw_stream(rng, 1_500_000)
             G = 8 // s["ch"]

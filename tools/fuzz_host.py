@@ -125,7 +125,11 @@ def main():
     stats = new_stats()
     bad = []
     deadline = time.monotonic() + args.seconds
+    tick = time.monotonic() + 30
     while time.monotonic() < deadline:
+        if time.monotonic() > tick:         # (a progress line every 30 s)
+            tick += 30
+            print("progress", json.dumps(stats), file=sys.stderr, flush=True)
         r = decode_round(rng, stats) if rng.random() < 0.75 else encode_round(rng, stats)
         if r is not None:
             bad.append(r)
