@@ -1274,13 +1274,20 @@ duplex_groups(std::vector<size_t> &first, size_t gm)
 	}
 }
 
-/* BJXA_DUPLEX_DIRECT=0: decodes always copy out through staging (read per
- * call, so one process can A/B it) */
+/*
+ * BJXA_DUPLEX_DIRECT=1: the copy-out kernel stores the output straight into
+ * the caller's buffer, registered for the call (read per call).  Opt-in: a
+ * randomised soak of the host API, run right after a long device-side one,
+ * ended with the card in a faulted state during a direct-route call, and
+ * the cause was not found; the default keeps the
+ * kernels' stores in runtime-allocated pinned staging and registers only
+ * the input, which only the copy engine reads.
+ */
 static bool
 duplex_direct(void)
 {
 	const char *e = getenv("BJXA_DUPLEX_DIRECT");
-	return e == NULL || strcmp(e, "0") != 0;
+	return e != NULL && strcmp(e, "1") == 0;
 }
 
 static std::mutex duplex_pool_mu;

@@ -43,9 +43,9 @@ ROUTES = ["direct", "staging"]
 
 
 def route_env(monkeypatch, route):
-    """The PCM straight into the registered caller buffer (direct, the
-    default for a resident 16-B aligned dst) or through pinned staging and
-    host copies (BJXA_DUPLEX_DIRECT=0, read per call)."""
+    """The output straight into the registered caller buffer (direct,
+    BJXA_DUPLEX_DIRECT=1, opt-in, for a resident 16-B aligned dst) or
+    through pinned staging and host copies (the default; read per call)."""
     monkeypatch.setenv("BJXA_DUPLEX_DIRECT", "1" if route == "direct" else "0")
 
 
@@ -278,12 +278,13 @@ def test_duplex_shared_input_pages(built):
 
 
 @pytest.mark.parametrize("case", ["fresh", "unaligned"])
-def test_duplex_output_placement(built, case):
-    """Outputs the direct route does not take: a freshly allocated buffer
-    whose pages were never touched (registering it would fault them all in
-    inside the call; xa_gpu.hip resident()) and one at a 2-byte offset (the
-    copy-out stores 16 B); both go through staging, bit-exact, nothing
-    written past the frames."""
+def test_duplex_output_placement(built, case, monkeypatch):
+    """Outputs the direct route (asked for here) does not take: a freshly
+    allocated buffer whose pages were never touched (registering it would
+    fault them all in inside the call; xa_gpu.hip resident()) and one at a
+    2-byte offset (the copy-out stores 16 B); both go through staging,
+    bit-exact, nothing written past the frames."""
+    route_env(monkeypatch, "direct")
     eb = 4 * slab_eblocks(2) + 321
     frames = eb * 32 - 5
     xa = synth.stream(eb, 8, 2, "A", seed=49)
@@ -304,10 +305,11 @@ def test_duplex_output_placement(built, case):
         assert (big[:2] == 0x5A).all() and (big[2 + n:] == 0x5A).all()
 
 
-def test_duplex_pinned_output(built):
+def test_duplex_pinned_output(built, monkeypatch):
     """An output buffer that is already pinned: registering it for the
-    direct route fails, the call goes back to staging before anything is
-    enqueued (duplex_run returns -2), same bytes."""
+    direct route (asked for here) fails, the call goes back to staging
+    before anything is enqueued (duplex_run returns -2), same bytes."""
+    route_env(monkeypatch, "direct")
     import torch
     eb = 4 * slab_eblocks(2) + 7
     xa = synth.stream(eb, 8, 2, "A", seed=51)

@@ -49,6 +49,9 @@ def decode_round(rng, stats, max_eb=2_500_000):
     bounds = [0] + cuts + [eb]
     out = np.full(eb * 64 * ch + 64, 0x3C, np.uint8)
     hdr = bjxa_amd.xa_header(xa.size, frames, 44100, bits, ch, state)
+    if os.environ.get("FUZZ_LOG"):
+        print("decode bits=%d ch=%d eb=%d mix=%s frames=%d bounds=%s bad=%d" % (
+            bits, ch, eb, mix, frames, bounds, badc), file=sys.stderr, flush=True)
     why = None
     failed = False
     with bjxa_amd.Decoder() as d:
@@ -90,6 +93,9 @@ def encode_round(rng, stats, max_frames=64_000_000):
     # block of source, src/libbjxa.c:778, ENOBUFS below it)
     frames = max(32, int(np.exp(rng.uniform(np.log(32), np.log(max_frames // ch)))))
     pcm = synth.pcm(frames, ch, seed=int(rng.integers(0, 1 << 30)))
+    if os.environ.get("FUZZ_LOG"):
+        print("encode bits=%d ch=%d frames=%d" % (bits, ch, frames), file=sys.stderr,
+              flush=True)
     e = bjxa_amd.Encoder()
     try:
         fmt = e.init({"data_len_pcm": frames * 2 * ch, "blocks": 0, "block_size_pcm": 0,
