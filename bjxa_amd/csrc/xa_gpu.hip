@@ -1614,15 +1614,16 @@ duplex_slot(const struct bjxa__gpu *g, size_t k, bool device)
  * enqueued.  Calls whose buffers share pages share or wait for each
  * other's registrations (reg_hold).
  *   in_range(k, &off, &len)    slab k's input bytes [off, off + len)
- *   gpu(k, ev, sd, ev_out)     enqueue slab k's kernel on sd (the decode
- *                              stream, after its input), record ev there,
- *                              and its copy-out (into the device view of
- *                              its staging slot, duplex_slot(), or
- *                              *d_direct) on g->s_out after ev, recording
- *                              ev_out[k] after it; a decode may hold back
- *                              a slab's kernel and copy-out to run them
- *                              with a later slab's (at most DUPLEX_SLOTS - 1
- *                              later); false on failure
+ *   gpu(k, sd, ev_dec)         enqueue slab k's kernel on sd (the decode
+ *                              stream, after its input) and record
+ *                              ev_dec[k] there; a decode may hold a slab
+ *                              back to run it with later slabs in one
+ *                              launch, recording every held slab's event
+ *                              then; false on failure
+ *   copy_out(k, ev, ev_out)    enqueue slab k's copy-out on g->s_out after
+ *                              ev (into the device view of its staging
+ *                              slot, duplex_slot(), or *d_direct) and
+ *                              record ev_out there; false on failure
  *   host(k, slot)              the calling thread's part once slab k's
  *                              copy-out is done: copy it out of its slot
  *                              (staging) or check its status; returns 1
@@ -1630,35 +1631,35 @@ duplex_slot(const struct bjxa__gpu *g, size_t k, bool device)
  *                              caller reports), -1 on failure
  * Returns 0 or -1/errno; every enqueued operation has finished on return.
  */
-template <class InRange, class Gpu, class Host>
+template <class InRange, class Gpu, class Out, class Host>
 static int
 duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
     uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
-    Gpu &&gpu, Host &&host);
+    Gpu &&gpu, Out &&copy_out, Host &&host);
 
 /* (the C ABI lets no exception out: allocations may fail before anything
  * is enqueued, and nothing after that throws) */
-template <class InRange, class Gpu, class Host>
+template <class InRange, class Gpu, class Out, class Host>
 static int
 duplex_run(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
     uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
-    Gpu &&gpu, Host &&host)
+    Gpu &&gpu, Out &&copy_out, Host &&host)
 {
 	*d_direct = NULL;
 	try {
 		return duplex_run_(g, n, src, in_bytes, out, out_bytes, d_direct,
-		    in_range, gpu, host);
+		    in_range, gpu, copy_out, host);
 	} catch (...) {
 		errno = ENOMEM;
 		return -1;
 	}
 }
 
-template <class InRange, class Gpu, class Host>
+template <class InRange, class Gpu, class Out, class Host>
 static int
 duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
     uint8_t *out, size_t out_bytes, uint8_t **d_direct, InRange &&in_range,
-    Gpu &&gpu, Host &&host)
+    Gpu &&gpu, Out &&copy_out, Host &&host)
 {
 	if (event_pool(g, 2 * n) < 0)	/* kernel done, copy-out done */
 		return -1;
@@ -1678,27 +1679,30 @@ duplex_run_(struct bjxa__gpu *g, size_t n, const uint8_t *src, size_t in_bytes,
 	}
 	if (out != NULL && *d_direct == NULL)
 		return -2;	/* nothing enqueued: the caller goes on without out */
+	/* every slab's input and kernel up front, on the decode stream: they
+	 * use no staging, and a kernel that runs beside a copy-out crawls but
+	 * is done long before its own copy-out is due */
 	uint8_t *d_in = (uint8_t *)g->d_in;
-	auto issue = [&](size_t k) -> bool {
+	bool ok = true;
+	for (size_t k = 0; ok && k < n; k++) {
 		size_t off, len;
 		in_range(k, &off, &len);
-		if (hipMemcpyAsync(d_in + off, src + off, len, hipMemcpyHostToDevice,
-		    g->s_dec) != hipSuccess)
-			return false;
+		ok = hipMemcpyAsync(d_in + off, src + off, len, hipMemcpyHostToDevice,
+		    g->s_dec) == hipSuccess && gpu(k, g->s_dec, ev_dec);
 		if (tr)
 			t_in[k] = trace_ms() - t0;
-		if (!gpu(k, ev_dec[k], g->s_dec, ev_out))
+	}
+	/* copy-outs in flight: as many as staging slots, or every slab when
+	 * the output is written directly (the host then reads only status
+	 * words, g->h_hst) */
+	auto issue = [&](size_t k) -> bool {
+		if (!copy_out(k, ev_dec[k], ev_out[k]))
 			return false;
 		if (tr)
 			t_iss[k] = trace_ms() - t0;
 		return true;
 	};
-
-	/* slabs in flight: as many as staging slots, or every slab when the
-	 * output is written directly (the host then reads only status words,
-	 * g->h_hst) */
 	const size_t depth = *d_direct != NULL ? n : (size_t)DUPLEX_SLOTS;
-	bool ok = true;
 	for (size_t k = 0; ok && k < std::min(n, depth); k++)
 		ok = issue(k);
 	for (size_t k = 0; ok && k < n; k++) {
@@ -1765,18 +1769,16 @@ duplex_decode(struct bjxa__gpu *g, const uint8_t *src, uint32_t eblocks,
 	uint32_t *stop = g->d_sst + g->sst_cap * XA_ST_WORDS;
 	uint8_t *d_dir = NULL;
 	int r;
-	/* (direct: every slab in flight, so any group size; staging: a group
-	 * must fit the DUPLEX_SLOTS slabs in flight.  Where the output cannot
-	 * be registered after all, duplex_run returns -2 before enqueueing
-	 * anything, and the call goes through staging) */
+	/* (where the output cannot be registered after all, duplex_run returns
+	 * -2 before enqueueing anything, and the call goes through staging) */
 again:
-	plan(direct ? gmax : std::min(gmax, (size_t)DUPLEX_SLOTS));
+	plan(gmax);
 	r = duplex_run(g, n, src, (size_t)eblocks * ebsz,
 	    direct ? dst : NULL, (size_t)dst_bytes, &d_dir,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ebsz;
 		*len = slab_eb(k) * ebsz;
-	}, [&](size_t k, hipEvent_t ev_done, hipStream_t sd, hipEvent_t *ev_out) -> bool {
+	}, [&](size_t k, hipStream_t sd, hipEvent_t *ev_dec) -> bool {
 		if (!last(k))
 			return true;	/* with the group's last slab */
 		const size_t a = first[k];
@@ -1795,11 +1797,23 @@ again:
 		 * previous group's */
 		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
 		if (decode_async(&s, g->d_ws, g->ws_cap, sst, NULL, sd,
-		    a > 0 ? g->d_sst + (a - 1) * XA_ST_WORDS : NULL) < 0 ||
-		    hipEventRecord(ev_done, sd) != hipSuccess ||
-		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
+		    a > 0 ? g->d_sst + (a - 1) * XA_ST_WORDS : NULL) < 0)
 			return false;
-		for (size_t j = a; j <= k; j++) {
+		for (size_t j = a; j <= k; j++)
+			if (hipEventRecord(ev_dec[j], sd) != hipSuccess)
+				return false;
+		return true;
+	}, [&](size_t j, hipEvent_t ev_done, hipEvent_t ev_o) -> bool {
+		/* slab j's copy-out; the status words are its decode group's,
+		 * which sit at the group's last slab */
+		const size_t a = first[j];
+		size_t k = j;
+		while (!last(k))
+			k++;
+		uint32_t *sst = g->d_sst + k * XA_ST_WORDS;
+		if (hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
+			return false;
+		{
 			const uint32_t ej = slab_eb(j);
 			const uint8_t *pj = (const uint8_t *)g->d_out + j * se * ob;
 			uint8_t *slot = duplex_slot(g, j, true);
@@ -1820,7 +1834,7 @@ again:
 				    (uint32_t *)slot);
 			}
 			if (hipGetLastError() != hipSuccess ||
-			    hipEventRecord(ev_out[j], g->s_out) != hipSuccess)
+			    hipEventRecord(ev_o, g->s_out) != hipSuccess)
 				return false;
 		}
 		return true;
@@ -1902,13 +1916,12 @@ duplex_encode(struct bjxa__gpu *g, const uint8_t *src, uint64_t frames,
 		return io_fail();
 	int r;
 again:
-	duplex_groups(first, direct ? duplex_egroup() :
-	    std::min(duplex_egroup(), (size_t)DUPLEX_SLOTS));
+	duplex_groups(first, duplex_egroup());
 	r = duplex_run(g, n, src, in_bytes, direct ? dst : NULL, xa_bytes, &d_dir,
 	    [&](size_t k, size_t *off, size_t *len) {
 		*off = k * se * ib;
 		*len = (size_t)slab_frames(k) * 2u * ch;
-	}, [&](size_t k, hipEvent_t ev_done, hipStream_t sd, hipEvent_t *ev_out) -> bool {
+	}, [&](size_t k, hipStream_t sd, hipEvent_t *ev_dec) -> bool {
 		if (!last(k))
 			return true;	/* with the group's last slab */
 		const size_t a = first[k];
@@ -1916,11 +1929,16 @@ again:
 		for (size_t j = a; j <= k; j++)
 			fg += slab_frames(j);
 		if (bjxa_hip_encode_async((uint8_t *)g->d_in + a * se * ib, fg, bits,
-		    ch, (uint8_t *)g->d_out + a * se * ebsz, sd) < 0 ||
-		    hipEventRecord(ev_done, sd) != hipSuccess ||
-		    hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
+		    ch, (uint8_t *)g->d_out + a * se * ebsz, sd) < 0)
 			return false;
-		for (size_t j = a; j <= k; j++) {
+		for (size_t j = a; j <= k; j++)
+			if (hipEventRecord(ev_dec[j], sd) != hipSuccess)
+				return false;
+		return true;
+	}, [&](size_t j, hipEvent_t ev_done, hipEvent_t ev_o) -> bool {
+		if (hipStreamWaitEvent(g->s_out, ev_done, 0) != hipSuccess)
+			return false;
+		{
 			uint8_t *slot = duplex_slot(g, j, true);
 			const size_t xk = (size_t)((slab_frames(j) + 31) / 32) * ebsz;
 			const uint4 *pj = (const uint4 *)((uint8_t *)g->d_out +
@@ -1942,7 +1960,7 @@ again:
 				    g->d_sst, (uint32_t *)slot);
 			}
 			if (hipGetLastError() != hipSuccess ||
-			    hipEventRecord(ev_out[j], g->s_out) != hipSuccess)
+			    hipEventRecord(ev_o, g->s_out) != hipSuccess)
 				return false;
 		}
 		return true;
