@@ -39,7 +39,13 @@ def host_decode(xa, eb, bits, ch, frames, state=(0, 0, 0, 0), fill=0x5A):
     return dst
 
 
-ROUTES = ["direct", "staging"]
+# the opt-in direct route (BJXA_DUPLEX_DIRECT=1) is tested on request
+# (BJXA_TEST_DIRECT=1): a fuzz run ended with a faulted card during one of
+# its calls, so the default suite stays on the
+# default route; its tests were green in every run of the round that asked
+ROUTES = ["staging", pytest.param("direct", marks=pytest.mark.skipif(
+    os.environ.get("BJXA_TEST_DIRECT") != "1",
+    reason="opt-in direct output route: set BJXA_TEST_DIRECT=1"))]
 
 
 def route_env(monkeypatch, route):
