@@ -1096,7 +1096,9 @@ call_buffers(struct bjxa__gpu *g, uint32_t eblocks, uint32_t ws_eblocks,
 #define DUPLEX_SLAB_MIB		16
 #endif
 #define DUPLEX_SLAB		((size_t)DUPLEX_SLAB_MIB << 20)	/* PCM bytes per slab */
+#ifndef DUPLEX_SLOTS
 #define DUPLEX_SLOTS		4
+#endif
 #define DUPLEX_HDR		4096			/* status, then the slab */
 #define DUPLEX_MIN_SLABS	(64 / DUPLEX_SLAB_MIB)	/* calls of >= 64 MiB of PCM */
 #define DUPLEX_OUT_CUS		64	/* the copy-out stream's CUs; 2 workgroups each */
