@@ -8,7 +8,9 @@ src/bjxa_decode.c:56-100) against the oracle: every format, ragged last
 slabs, cut last blocks, header entry states, a call chained after another,
 and the EPROTO semantics of test/test_decode_error.sh:221-282 with the bad
 block in a middle slab; BJXA_DUPLEX=0 (the serial route) gives the same
-bytes."""
+bytes.  The default output route is pinned staging; the opt-in direct
+route (BJXA_DUPLEX_DIRECT=1, the output registered and written by the
+copy-out kernel) is tested when BJXA_TEST_DIRECT=1 is set."""
 import errno
 import os
 import subprocess
